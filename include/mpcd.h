@@ -1,0 +1,178 @@
+/*
+ * mpcd.h — C ABI of libmpcd.so, the MI355X (gfx950) diffusion-MPC hot path.
+ *
+ * The reference (XuehuaOvO/MPC_via_Diffusion_Model) is pure Python/PyTorch; its seam for this
+ * path is a Python call, not an FFI. Each entry point below replaces one reference interface
+ * (cited file:line, paths relative to the reference root); the Python package
+ * mpc_via_diffusion_model_amd binds them with ctypes.
+ *
+ * Conventions
+ *  - Every function returns 0 (MPCD_OK) or a negative mpcd_status; nothing throws across the ABI.
+ *    mpcd_last_error() gives a thread-local message for the last failure on this thread.
+ *  - "dev" pointers are device (HBM) pointers owned by the caller; "host" pointers are read
+ *    during the call only. Weights, schedule, plan and workspace belong to the context.
+ *  - Work is enqueued on the caller's HIP stream (void* hip_stream; NULL = legacy default stream)
+ *    and is asynchronous unless stated otherwise. One context per device; not thread-safe.
+ *  - All trajectory tensors are fp32 row-major [B][H][d] (candidate, horizon, action dim), the
+ *    layout of the reference's x in cart_pole_sample_loop (diffusion_model_base.py:188-189).
+ */
+#ifndef MPCD_H
+#define MPCD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mpcd_ctx mpcd_ctx;
+
+enum mpcd_status {
+    MPCD_OK = 0,
+    MPCD_EINVAL = -1,   /* bad argument / shape */
+    MPCD_EHIP = -2,     /* HIP runtime error */
+    MPCD_ESTATE = -3,   /* missing net / schedule, or call out of order */
+    MPCD_ENOMEM = -4,
+    MPCD_EUNSUP = -5,   /* configuration the kernels do not implement */
+};
+
+enum mpcd_net_kind {
+    MPCD_NET_MLP = 1,   /* build-defined CFG MLP noise-net: PointUnet stack on [B, H*d] (temporal_unet.py:451-550) */
+    MPCD_NET_UNET = 2,  /* ConditionedTemporalUnet (temporal_unet.py:189-358) or TemporalUnet (:28-187) */
+};
+
+enum mpcd_dtype { MPCD_F32 = 0, MPCD_F16 = 1 };
+
+typedef struct {
+    int32_t kind;          /* mpcd_net_kind */
+    int32_t state_dim;     /* d: channels of the denoised trajectory (actions per horizon point) */
+    int32_t horizon;       /* H (MLP: input width H*d; UNet: H % 4 == 0) */
+    int32_t context_dim;   /* C: conditioning width (0 = TemporalUnet with conditioning None) */
+    int32_t base_dim;      /* unet_input_dim / dim, 32 */
+    int32_t n_mults;       /* len(dim_mults), 3 for UNET_DIM_MULTS[0] = (1, 2, 4) */
+    int32_t mults[4];
+    int32_t time_emb_dim;  /* 32 */
+    int32_t cfg_masked;    /* 1: 4-arg net with the CFG context mask (ConditionedTemporalUnet :296-300);
+                              0: 3-arg TemporalUnet (context concatenated unmasked when C > 0) */
+    int32_t dtype;         /* mpcd_dtype of the hidden activations/GEMM operands */
+} mpcd_net_desc;
+
+/* Parameter blob = every parameter of the torch module, flattened row-major, concatenated in the
+ * order mpcd_net_param_info() enumerates (= the module's state_dict() order, which is the
+ * reference's for the U-Nets, e.g. "time_mlp.encoder.1.weight", "downs.0.0.blocks.0.block.0.weight").
+ * Replaces GaussianDiffusionModel(model=...) + load_state_dict (Diffusion_MPC_Inference.py:211-222). */
+int mpcd_net_param_count(const mpcd_net_desc *desc, int32_t *n_tensors, int64_t *n_floats);
+int mpcd_net_param_info(const mpcd_net_desc *desc, int32_t i, char *name, size_t name_cap,
+                        int32_t *ndim, int64_t shape[4]);
+
+int mpcd_create(int device, mpcd_ctx **out);
+void mpcd_destroy(mpcd_ctx *ctx);
+const char *mpcd_last_error(void);
+
+/* Upload and repack weights into the kernels' layouts (blocking). */
+int mpcd_load_net(mpcd_ctx *ctx, const mpcd_net_desc *desc, const float *blob_host, size_t n_floats);
+
+/* The 12 diffusion buffers, fp32, each [n_steps], in GaussianDiffusionModel's registration order
+ * (diffusion_model_base.py:87-109): betas, alphas_cumprod, alphas_cumprod_prev, sqrt_alphas_cumprod,
+ * sqrt_one_minus_alphas_cumprod, log_one_minus_alphas_cumprod, sqrt_recip_alphas_cumprod,
+ * sqrt_recipm1_alphas_cumprod, posterior_variance, posterior_log_variance_clipped,
+ * posterior_mean_coef1, posterior_mean_coef2.
+ * posterior_std_host: optional [n_steps] = sqrt(exp(posterior_log_variance_clipped)) as the caller's
+ * fp32 math computes it (sample_functions.py:35-37); NULL = computed here with expf/sqrtf. */
+int mpcd_set_schedule(mpcd_ctx *ctx, const float *tables_host, int32_t n_steps, const float *posterior_std_host);
+
+enum mpcd_sampler {
+    MPCD_DDPM_CFG = 0,  /* run_CFG + ddpm_cart_pole_sample_fn (diffusion_model_base.py:394-418, sample_functions.py:17-44) */
+    MPCD_DDIM_CFG = 1,  /* build-defined CFG-DDIM */
+    MPCD_DDIM = 2,      /* ddim_sample with a 3-arg net (diffusion_model_base.py:239-314), eta = 0 */
+};
+
+typedef struct {
+    const float *context;      /* dev [B][C] normalised context, or [1][C] if context_shared; NULL if C == 0 */
+    int32_t context_shared;    /* 1: one context row for every candidate (one x0 per control step) */
+    int32_t sampler;           /* mpcd_sampler */
+    int64_t batch;             /* B candidates handled by this call (this rank's shard) */
+    double w;                  /* CFG weight (context_weight of run_CFG) */
+    int32_t n_wo_noise;        /* n_diffusion_steps_without_noise (DDPM) */
+    int32_t ddim_steps;        /* DDIM sampling_timesteps; 0 = reference n_steps // 5 (:252) */
+    int32_t clamp_x0;          /* DDIM only; DDPM always clamps (clip_denoised, :172-173) */
+    int32_t n_ddim_times;      /* length of ddim_times, 0 = derive the grid here */
+    const int32_t *ddim_times; /* host, optional: the reference's time list [T-1, ..., 0, -1] (:255-258) */
+    uint64_t seed;             /* Philox4x32-10 key (throughput mode) */
+    int64_t global_offset;     /* global index of candidate 0 (Philox counter; sharding-invariant) */
+    const float *noise;        /* dev [S+1][B][H][d] injected noise (parity mode) or NULL -> Philox;
+                                  slice 0 = x_T, slice k = the draw of denoise step k */
+    float *x_out;              /* dev [B][H][d] final normalised sample */
+    float *chain_out;          /* dev [S+1][B][H][d] or NULL (run_CFG return_chain, :403-415) */
+} mpcd_sample_args;
+
+/* Number of denoise steps S a call makes (DDPM: N + n_wo_noise; DDIM: grid pairs). */
+int mpcd_sample_steps(mpcd_ctx *ctx, const mpcd_sample_args *args, int32_t *n_steps);
+int mpcd_sample(mpcd_ctx *ctx, const mpcd_sample_args *args, void *hip_stream);
+
+/* One noise-net forward at diffusion time t (the model(x, t, context, mask) calls of
+ * p_mean_variance_CFG, diffusion_model_base.py:166-168): x dev [B][H][d]; eps_cond dev [B][H][d] =
+ * net(x, t, ctx, mask = 0); eps_uncond dev [B][H][d] = net(x, t, ctx, mask = 1) for a cfg_masked net
+ * (NULL for a 3-arg net, whose single output goes to eps_cond). */
+int mpcd_eps(mpcd_ctx *ctx, const float *x, int32_t t, const float *context, int32_t context_shared, int64_t batch,
+             float *eps_cond, float *eps_uncond, void *hip_stream);
+
+/* --- rollout / cost / selection --- */
+enum mpcd_system {
+    MPCD_SYS_CARTPOLE_LIN5 = 0,  /* EulerForwardCartpole_virtual, Cart_Diffusion_inference.py:168-197 */
+    MPCD_SYS_CARTPOLE_NL5 = 1,   /* nonlinear Euler, nmpc_multi_process_collect_data.py:121-137 */
+    MPCD_SYS_CARTPOLE_ZOH4 = 2,  /* linear ZOH, Diffusion_MPC_Inference.py:39-84 */
+    MPCD_SYS_DOUBLE_INT2D = 3,   /* build-defined */
+    MPCD_SYS_PENDULUM = 4,       /* build-defined */
+    MPCD_SYS_QUADROTOR12 = 5,    /* build-defined */
+};
+enum mpcd_cost_kind {
+    MPCD_COST_CANONICAL = 0,     /* J = q(x0) + sum_k [q(x_{k+1}) + r(u_k)], terminal P (nmpc...py:158-172) */
+    MPCD_COST_CALMPC = 1,        /* calMPCCost quirks (Cart_Diffusion_inference.py:247-283) */
+};
+
+typedef struct {
+    int32_t system;      /* mpcd_system */
+    int32_t cost_kind;   /* mpcd_cost_kind */
+    int32_t n_x, n_u;    /* n_u must equal the net's state_dim */
+    double params[24];   /* dynamics constants, layout per system (mpc_via_diffusion_model_amd/systems.py) */
+    double Q[12], R[4], P[12], x_ref[12];   /* diagonal weights and set-point, fp64 */
+} mpcd_system_desc;
+
+/* Global clip flag of LimitsNormalizer.unnormalize (normalization.py:160-162): *flag_dev = 1 iff some
+ * x[i] > 1+1e-4 or < -1-1e-4 over the n values, else 0. Sharded callers OR the per-rank flags. */
+int mpcd_clip_flag(mpcd_ctx *ctx, const float *x, int64_t n, int32_t *flag_dev, void *hip_stream);
+
+/* Unnormalise (LimitsNormalizer.unnormalize, normalization.py:156-167; clip iff the GLOBAL max/min of
+ * u_norm leaves [-1-1e-4, 1+1e-4]) then roll out and cost every candidate in fp64, one thread each.
+ * x0_host [n_x] fp64; u_norm dev [B][H][n_u]; umin/umax host [n_u] fp32 (dataset limits);
+ * clip_flag_dev: dev int32 from mpcd_clip_flag (e.g. OR-reduced over ranks), or NULL = computed here
+ * from u_norm; cost_out dev [B] fp64. Replaces calMPCCost / the MPC objective evaluated per sample. */
+int mpcd_rollout_cost(mpcd_ctx *ctx, const mpcd_system_desc *sys, const double *x0_host, const float *u_norm,
+                      const float *umin_host, const float *umax_host, int64_t batch, int32_t horizon,
+                      const int32_t *clip_flag_dev, double *cost_out, void *hip_stream);
+
+/* Unnormalise only: out = ((x+1)/2)*(max-min)+min in fp32 over [n_rows][dim], with the global clip
+ * rule (clip_flag_dev as above; NULL = computed from x). dim <= 16. */
+int mpcd_unnormalize(mpcd_ctx *ctx, const float *x, int64_t n_rows, int32_t dim, const float *min_host,
+                     const float *max_host, const int32_t *clip_flag_dev, float *out, void *hip_stream);
+
+typedef struct {
+    double cost;         /* +inf if every cost is NaN */
+    int64_t index;       /* index_offset + position; lowest index on ties; NaN costs rank as +inf */
+} mpcd_best;
+
+/* Device argmin over cost[n] (torch.argmin(cost_all), inference_(mpd).py:335-338). best_dev is a
+ * device pointer to one mpcd_best. */
+int mpcd_argmin(mpcd_ctx *ctx, const double *cost, int64_t n, int64_t index_offset, mpcd_best *best_dev,
+                void *hip_stream);
+
+/* Timing of the last mpcd_sample's main kernel (HIP events on the call's stream), milliseconds.
+ * Blocks until that kernel has finished. */
+int mpcd_last_sample_ms(mpcd_ctx *ctx, float *ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCD_H */

@@ -1,0 +1,116 @@
+"""ctypes binding of libmpcd.so (include/mpcd.h).
+
+The product path has no fallback: if the library is missing or a call fails, this raises.
+torch is imported first so the process has exactly one HIP runtime (torch's libamdhip64.so.7,
+which the library's DT_NEEDED entry then resolves to).
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before libmpcd.so)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmpcd.so")
+
+MPCD_NET_MLP, MPCD_NET_UNET = 1, 2
+MPCD_F32, MPCD_F16 = 0, 1
+MPCD_DDPM_CFG, MPCD_DDIM_CFG, MPCD_DDIM = 0, 1, 2
+MPCD_COST_CANONICAL, MPCD_COST_CALMPC = 0, 1
+
+_STATUS = {-1: "EINVAL", -2: "EHIP", -3: "ESTATE", -4: "ENOMEM", -5: "EUNSUP"}
+
+
+class NetDesc(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("state_dim", ctypes.c_int32), ("horizon", ctypes.c_int32),
+                ("context_dim", ctypes.c_int32), ("base_dim", ctypes.c_int32), ("n_mults", ctypes.c_int32),
+                ("mults", ctypes.c_int32 * 4), ("time_emb_dim", ctypes.c_int32), ("cfg_masked", ctypes.c_int32),
+                ("dtype", ctypes.c_int32)]
+
+
+class SampleArgs(ctypes.Structure):
+    _fields_ = [("context", ctypes.c_void_p), ("context_shared", ctypes.c_int32), ("sampler", ctypes.c_int32),
+                ("batch", ctypes.c_int64), ("w", ctypes.c_double), ("n_wo_noise", ctypes.c_int32),
+                ("ddim_steps", ctypes.c_int32), ("clamp_x0", ctypes.c_int32), ("n_ddim_times", ctypes.c_int32),
+                ("ddim_times", ctypes.POINTER(ctypes.c_int32)), ("seed", ctypes.c_uint64),
+                ("global_offset", ctypes.c_int64), ("noise", ctypes.c_void_p), ("x_out", ctypes.c_void_p),
+                ("chain_out", ctypes.c_void_p)]
+
+
+class SystemDesc(ctypes.Structure):
+    _fields_ = [("system", ctypes.c_int32), ("cost_kind", ctypes.c_int32), ("n_x", ctypes.c_int32),
+                ("n_u", ctypes.c_int32), ("params", ctypes.c_double * 24), ("Q", ctypes.c_double * 12),
+                ("R", ctypes.c_double * 4), ("P", ctypes.c_double * 12), ("x_ref", ctypes.c_double * 12)]
+
+
+class Best(ctypes.Structure):
+    _fields_ = [("cost", ctypes.c_double), ("index", ctypes.c_int64)]
+
+
+EXPORTS = {
+    "mpcd_net_param_count": ([ctypes.POINTER(NetDesc), ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)],
+                             ctypes.c_int),
+    "mpcd_net_param_info": ([ctypes.POINTER(NetDesc), ctypes.c_int32, ctypes.c_char_p, ctypes.c_size_t,
+                             ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
+    "mpcd_create": ([ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "mpcd_destroy": ([ctypes.c_void_p], None),
+    "mpcd_last_error": ([], ctypes.c_char_p),
+    "mpcd_load_net": ([ctypes.c_void_p, ctypes.POINTER(NetDesc), ctypes.c_void_p, ctypes.c_size_t], ctypes.c_int),
+    "mpcd_set_schedule": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p], ctypes.c_int),
+    "mpcd_sample_steps": ([ctypes.c_void_p, ctypes.POINTER(SampleArgs), ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+    "mpcd_sample": ([ctypes.c_void_p, ctypes.POINTER(SampleArgs), ctypes.c_void_p], ctypes.c_int),
+    "mpcd_eps": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
+                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "mpcd_clip_flag": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p],
+                       ctypes.c_int),
+    "mpcd_rollout_cost": ([ctypes.c_void_p, ctypes.POINTER(SystemDesc), ctypes.c_void_p, ctypes.c_void_p,
+                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
+                           ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "mpcd_unnormalize": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
+                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "mpcd_argmin": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                     ctypes.c_void_p], ctypes.c_int),
+    "mpcd_last_sample_ms": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+}
+
+_lib = None
+
+
+class MpcdError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libmpcd.so (raises if it was not built: there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MpcdError(f"{LIB_PATH} is missing: run `python -m mpc_via_diffusion_model_amd.build` "
+                            "(the HIP library is required; there is no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (argt, rest) in EXPORTS.items():
+            fn = getattr(L, name)
+            fn.argtypes = argt
+            fn.restype = rest
+        _lib = L
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().mpcd_last_error().decode(errors="replace")
+        raise MpcdError(f"{what} failed ({_STATUS.get(rc, rc)}): {msg}")
+
+
+def param_spec(desc):
+    """[(name, shape)] in blob order, straight from the library (single source of truth)."""
+    L = lib()
+    n_t, n_f = ctypes.c_int32(), ctypes.c_int64()
+    check(L.mpcd_net_param_count(ctypes.byref(desc), ctypes.byref(n_t), ctypes.byref(n_f)), "mpcd_net_param_count")
+    out = []
+    buf = ctypes.create_string_buffer(256)
+    nd = ctypes.c_int32()
+    shp = (ctypes.c_int64 * 4)()
+    for i in range(n_t.value):
+        check(L.mpcd_net_param_info(ctypes.byref(desc), i, buf, 256, ctypes.byref(nd), shp), "mpcd_net_param_info")
+        out.append((buf.value.decode(), tuple(shp[k] for k in range(nd.value))))
+    return out

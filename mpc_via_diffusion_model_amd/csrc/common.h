@@ -1,0 +1,81 @@
+// Shared device helpers for the gfx950 kernels of libmpcd.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MPCD_DEV __device__ __forceinline__
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte load through an explicit global (addrspace 1) pointer: global_load_dwordx4, never flat_
+// (a flat load also counts on lgkmcnt and forces full drains around LDS waits).
+typedef const float __attribute__((address_space(1))) *gptr_f;
+MPCD_DEV f32x4 ldg4(const float *p) { return *reinterpret_cast<const f32x4 __attribute__((address_space(1))) *>((gptr_f)p); }
+
+// LDS-only workgroup barrier: retire this wave's LDS traffic, then s_barrier, in ONE asm
+// statement so no memory access can be moved across it, and without the vmcnt(0) a
+// __syncthreads() fence may add (register-destination global prefetches stay in flight).
+MPCD_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Mish(x) = x * tanh(softplus(x)) (torch.nn.Mish). With n = e^x,
+// tanh(log1p(n)) = n(n+2) / (n(n+2) + 2): one exp and one divide; for x > 20 the factor is 1 in fp32.
+// Accuracy matters more than it looks: the error of every Mish feeds the next layer, and twelve of
+// them sit between x and eps. expf (ocml, ~1 ulp) and an IEEE divide keep the whole net within a
+// few 1e-8 of an fp64 forward; the __expf (v_exp_f32 on x*log2e) shortcut cost ~1e-6.
+MPCD_DEV float mish(float x)
+{
+    const float n = expf(x);
+    const float p = n * (n + 2.0f);
+    const float r = p / (p + 2.0f);
+    return x > 20.0f ? x : x * r;
+}
+
+// Philox4x32-10 (Salmon et al., SC'11). counter/key -> 4 uniform uint32.
+MPCD_DEV uint4 philox4x32_10(uint4 c, uint2 k)
+{
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+        const uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+        k.x += W0;
+        k.y += W1;
+    }
+    return c;
+}
+
+// Four standard normals for (seed, candidate, step, element quad) via Box-Muller.
+MPCD_DEV f32x4 philox_normal4(uint64_t seed, uint64_t cand, uint32_t step, uint32_t quad)
+{
+    const uint4 r = philox4x32_10(make_uint4(quad, (uint32_t)cand, (uint32_t)(cand >> 32), step),
+                                  make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+    const float s = 2.3283064365386963e-10f;  // 2^-32
+    const float u0 = ((float)r.x + 1.0f) * s, u1 = (float)r.y * s;
+    const float u2 = ((float)r.z + 1.0f) * s, u3 = (float)r.w * s;
+    const float ra = __fsqrt_rn(-2.0f * __logf(u0)), rb = __fsqrt_rn(-2.0f * __logf(u2));
+    const float ta = 6.2831853071795865f * u1, tb = 6.2831853071795865f * u3;
+    f32x4 z;
+    z.x = ra * __cosf(ta);
+    z.y = ra * __sinf(ta);
+    z.z = rb * __cosf(tb);
+    z.w = rb * __sinf(tb);
+    return z;
+}
+
+// One denoise step of the plan (built on the host from the schedule buffers).
+struct StepPlan {
+    int32_t t;        // network time index
+    int32_t flags;    // bit0: add noise (DDPM t > 0); bit1: final DDIM pair (x <- x0)
+    float a, b;       // sqrt_recip_alphas_cumprod[t], sqrt_recipm1_alphas_cumprod[t]
+    float c1, c2;     // posterior_mean_coef1/2[t] (DDPM)
+    float std;        // sqrt(exp(posterior_log_variance_clipped[t])) (DDPM)
+    float sqan, cn;   // sqrt(abar_next), sqrt(1 - abar_next - sigma^2) (DDIM)
+    float pad;
+};
+static_assert(sizeof(StepPlan) == 40, "StepPlan layout");
+
+enum { PLAN_NOISE = 1, PLAN_FINAL = 2 };
+enum { MODE_DDPM_CFG = 0, MODE_DDIM_CFG = 1, MODE_DDIM = 2, MODE_EPS = 3, MODE_EPS1 = 4 };
+// MODE_EPS / MODE_EPS1: one net forward at plan[0].t on x = noise[0]; eps of the context branch ->
+// x_out, of the masked branch -> chain (MODE_EPS, CFG net) or just x_out (MODE_EPS1, 3-arg net).

@@ -1,0 +1,47 @@
+// Internal (non-ABI) declarations shared by the libmpcd.so translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+
+// One conditioning Linear (cond_mlp.1 of a residual / MLP block): out width `width`, weight
+// [width][cond_dim] row-major, written at column `off` of the per-step / per-candidate tables.
+struct CondLayer {
+    const float *W;
+    const float *b;
+    int32_t width;
+    int32_t off;
+};
+
+// Time-embedding prologue: tproj[s][off_j + n] = cond_mlp_j.W[n, :T] . Mish(t_emb(t_s)) + b_j[n]
+void launch_time_prologue(const StepPlan *plan, int n_steps, const float *time_w1, const float *time_b1,
+                          const float *time_w2, const float *time_b2, const CondLayer *layers_dev, int n_layers,
+                          int cond_dim, int cond_total, float *tproj, hipStream_t stream);
+
+// Context prologue: cproj[b][off_j + n] = cond_mlp_j.W[n, T:] . Mish(ctx_b)   (no bias)
+void launch_ctx_prologue(const float *ctx, int64_t n_rows, int ctx_dim, const CondLayer *layers_dev, int n_layers,
+                         int cond_dim, int cond_total, float *cproj, hipStream_t stream);
+
+struct MlpSampleArgs {
+    const float *wpack;      // packed linear layers (see mlp_sampler.hip)
+    const StepPlan *plan;    // [S]
+    const float *tproj;      // [S][448]
+    const float *cproj;      // [B or 1][448] or null (no context / NB == 1 unconditioned)
+    int64_t cproj_stride;    // 448 or 0 (shared context)
+    const float *noise;      // [S+1][B][D0] or null
+    float *x_out;            // [B][D0]
+    float *chain;            // [S+1][B][D0] or null
+    int64_t batch;
+    int64_t global_offset;
+    uint64_t seed;
+    int32_t n_steps;
+    int32_t mode;            // MODE_*
+    int32_t clamp_x0;
+    float wp1, wf;           // fp32(1 + w), fp32(w)
+    float *dbg;              // debug: block 0 dumps every layer output [14][32][256] (null in production)
+};
+
+int mlp_packed_floats(int d0);
+void mlp_pack_weights(int d0, const float *const *lin_w, const float *const *lin_b, float *out);
+hipError_t launch_mlp_sampler(int d0, int nb, const MlpSampleArgs &a, hipStream_t stream);

@@ -1,0 +1,521 @@
+// Persistent CFG-DDPM / DDIM sampler for the MLP noise-net on gfx950.
+//
+// One launch runs every denoise step for every candidate. A 256-thread
+// workgroup owns 32 "rows": for CFG (NB = 2) 16 candidates x {context, masked context}
+// (the two forwards of p_mean_variance_CFG, diffusion_model_base.py:164-178, batched as rows),
+// for the 3-arg net (NB = 1) 32 candidates. Activations never leave LDS; the trajectory x stays
+// in LDS across all steps; weights stream from L2 into VGPRs one layer ahead of use.
+//
+// Net (build-defined CFG MLP, SURVEY §8a A11 = PointUnet temporal_unet.py:489-550 on [B, H*d]):
+//   6 TemporalBlockMLP (layers.py:358-385): y = Mish(L2(Mish(L1 x)) + cond_mlp(c)); downs 3,
+//   mid 1, ups 2 with cat(x, skip); final MLP(32, H*d, act=identity) = 2 Linear. 14 Linear total.
+// cond_mlp(c) = Linear(Mish(cat(t_emb, ctx))) is split exactly into a per-step table (time part +
+// bias, tproj) and a per-candidate table (context part, cproj) built by the prologue kernels.
+//
+// GEMM: D = W . act^T on v_mfma_f32_16x16x4_f32 (exact f32, fmaf-chain numerics): A = W rows (out
+// features), B = activation rows. A lane's float4 of W and float4 of act cover 4 k each, so one
+// 16-k block = 4 MFMAs; the k permutation is the same for A and B. Output lane layout: 4 consecutive
+// features of one row -> one ds_write_b128.
+#include <hip/hip_runtime.h>
+
+#include "internal.h"
+
+namespace {
+
+constexpr int ROWS = 32;
+constexpr int THREADS = 256;
+constexpr int NLAYER = 14;
+constexpr int COND_TOTAL = 448;  // 32+64+128+128+64+32
+enum { EPI_NONE = 0, EPI_MISH = 1, EPI_CMISH = 2 };
+enum { SPLIT = 0, PAIRED = 1 };
+
+template <int D0>
+struct Arch {
+    static constexpr int K[NLAYER] = {D0, 32, 32, 64, 64, 128, 128, 128, 256, 64, 128, 32, 32, 32};
+    static constexpr int N[NLAYER] = {32, 32, 64, 64, 128, 128, 128, 128, 64, 64, 32, 32, 32, D0};
+    static constexpr int woff(int l) { return l == 0 ? 0 : woff(l - 1) + K[l - 1] * N[l - 1] + N[l - 1]; }
+    static constexpr int total() { return woff(NLAYER); }
+};
+
+// cond block j (0..5) -> column offset in the 448-wide tables
+__host__ __device__ constexpr int cond_off(int j) { return j == 0 ? 0 : j == 1 ? 32 : j == 2 ? 96 : j == 3 ? 224 : j == 4 ? 352 : 416; }
+
+// ---- LDS layout (floats). Row strides are width + 4 so the 16 rows a ds_read_b128 lane group
+// touches land on different 16-byte bank slots.
+template <int D0, int NB>
+struct Lds {
+    static constexpr int CPW = ROWS / NB;          // candidates per workgroup
+    static constexpr int SX = D0 + 4, ST1 = 132, SS1 = 36, SC1 = 132, SC0 = 260;
+    static constexpr int XB = 0;
+    static constexpr int T1 = XB + CPW * SX;
+    static constexpr int S1 = T1 + ROWS * ST1;
+    static constexpr int C1 = S1 + ROWS * SS1;
+    static constexpr int C0 = C1 + ROWS * SC1;
+    static constexpr int TP = C0 + ROWS * SC0;     // this step's tproj [448]
+    static constexpr int CP = TP + COND_TOTAL;     // per-candidate cproj [CPW][448]
+    static constexpr int total(bool ctx) { return CP + (ctx ? CPW * COND_TOTAL : 0); }
+};
+
+template <int N>
+constexpr int mode_for() { return N == 32 ? SPLIT : PAIRED; }
+
+template <int K, int N, int MODE>
+struct WFrag {
+    static constexpr int NT = N / 16;
+    static constexpr int T = MODE == SPLIT ? NT / 2 : (NT + 3) / 4;
+    static constexpr int KB = K / 16;
+    f32x4 v[T][KB];
+};
+
+template <int K, int N, int MODE>
+MPCD_DEV int ntile_of(int wave, int j)
+{
+    return MODE == SPLIT ? (wave >> 1) + 2 * j : wave + 4 * j;
+}
+
+template <int K, int N, int MODE>
+MPCD_DEV void load_w(WFrag<K, N, MODE> &f, const float *__restrict__ wp, int wave, int lane)
+{
+    constexpr int KB = K / 16, NT = N / 16;
+#pragma unroll
+    for (int j = 0; j < WFrag<K, N, MODE>::T; ++j) {
+        const int nt = ntile_of<K, N, MODE>(wave, j);
+        if (MODE == PAIRED && NT % 4 != 0 && nt >= NT) continue;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+            f.v[j][kb] = ldg4(wp + ((size_t)(nt * KB + kb) * 64 + lane) * 4);
+    }
+}
+
+MPCD_DEV f32x4 mfma4(const f32x4 &w, const f32x4 &a, f32x4 acc)
+{
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, a.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, a.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, a.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, a.w, acc, 0, 0, 0);
+    return acc;
+}
+
+// Hidden layer. SPLIT (N = 32): wave w -> column tile (w & 1), n-tiles (w >> 1) + 2j.
+// PAIRED (N >= 64): wave w -> n-tiles w + 4j for BOTH column tiles, so each weight register feeds
+// two MFMAs and a wave holds only a quarter of the layer's weights.
+// in_shared: both column tiles read rows 0..15 (layer 0 with CFG: both branches see the same x).
+template <int K, int N, int MODE, int EPI, int NB>
+MPCD_DEV void hidden_layer(const WFrag<K, N, MODE> &f, const float *__restrict__ bias, const float *in, int in_stride,
+                           bool in_shared, float *out, int out_stride, const float *tp, const float *cp, int cond_j,
+                           bool has_ctx, int wave, int lane)
+{
+    constexpr int T = WFrag<K, N, MODE>::T, KB = K / 16, NT = N / 16;
+    constexpr int NCT = MODE == SPLIT ? 1 : 2;
+    const int col = lane & 15, q = lane >> 4;
+    const float *arow[NCT];
+#pragma unroll
+    for (int c = 0; c < NCT; ++c) {
+        const int ct = MODE == SPLIT ? (wave & 1) : c;
+        arow[c] = in + (size_t)((in_shared ? 0 : ct * 16) + col) * in_stride + 4 * q;
+    }
+    f32x4 acc[T][NCT];
+#pragma unroll
+    for (int j = 0; j < T; ++j)
+#pragma unroll
+        for (int c = 0; c < NCT; ++c) acc[j][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+        f32x4 a[NCT];
+#pragma unroll
+        for (int c = 0; c < NCT; ++c) a[c] = *reinterpret_cast<const f32x4 *>(arow[c] + kb * 16);
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            if (MODE == PAIRED && NT % 4 != 0 && ntile_of<K, N, MODE>(wave, j) >= NT) continue;
+#pragma unroll
+            for (int c = 0; c < NCT; ++c) acc[j][c] = mfma4(f.v[j][kb], a[c], acc[j][c]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < T; ++j) {
+        const int nt = ntile_of<K, N, MODE>(wave, j);
+        if (MODE == PAIRED && NT % 4 != 0 && nt >= NT) continue;
+        const int n = nt * 16 + 4 * q;
+        const f32x4 b4 = ldg4(bias + n);
+        f32x4 tc = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (EPI == EPI_CMISH) tc = *reinterpret_cast<const f32x4 *>(tp + cond_off(cond_j) + n);
+#pragma unroll
+        for (int c = 0; c < NCT; ++c) {
+            const int ct = MODE == SPLIT ? (wave & 1) : c;
+            const int row = ct * 16 + col;
+            f32x4 v = acc[j][c] + b4;
+            if (EPI == EPI_CMISH) {
+                // NB == 2: column tile = branch (0: context, 1: masked -> time part only); NB == 1: all unmasked.
+                // Branch-free select (the masked rows take tc exactly): a wave-uniform branch around this
+                // LDS load let the masked rows consume a stale .w register (seen on gfx950 / ROCm 7.2).
+                f32x4 cv = tc;
+                if (has_ctx) {
+                    const int cand = NB == 2 ? col : row;
+                    const f32x4 cpv = *reinterpret_cast<const f32x4 *>(cp + cand * COND_TOTAL + cond_off(cond_j) + n);
+                    const f32x4 sum = tc + cpv;
+                    const bool take = NB == 1 || ct == 0;
+                    cv.x = take ? sum.x : tc.x;
+                    cv.y = take ? sum.y : tc.y;
+                    cv.z = take ? sum.z : tc.z;
+                    cv.w = take ? sum.w : tc.w;
+                }
+                v = v + cv;
+            }
+            if (EPI != EPI_NONE) {
+                v.x = mish(v.x);
+                v.y = mish(v.y);
+                v.z = mish(v.z);
+                v.w = mish(v.w);
+            }
+            *reinterpret_cast<f32x4 *>(out + (size_t)row * out_stride + n) = v;
+        }
+    }
+}
+
+template <int D0, int SMODE, bool CTX>
+struct MlpKernel {
+    static constexpr int NB = (SMODE == MODE_DDIM || SMODE == MODE_EPS1) ? 1 : 2;
+    using A = Arch<D0>;
+    using L = Lds<D0, NB>;
+    static constexpr int CPW = L::CPW;
+    static constexpr int QUADS = D0 / 4;  // float4 quads per candidate trajectory
+
+    // final Linear (32 -> D0) in PAIRED mode + the denoise update, x kept in LDS
+    static MPCD_DEV void final_and_update(const WFrag<32, D0, PAIRED> &f, const float *__restrict__ bias, float *lds,
+                                          const MlpSampleArgs &p, const StepPlan &sp, int s, int64_t cand0,
+                                          const f32x4 (&nz)[WFrag<32, D0, PAIRED>::T][NB], int wave, int lane)
+    {
+        constexpr int T = WFrag<32, D0, PAIRED>::T, NT = D0 / 16;
+        const int col = lane & 15, q = lane >> 4;
+        f32x4 acc[T][2];
+#pragma unroll
+        for (int j = 0; j < T; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+            const float *arow = lds + L::T1 + (size_t)(ct * 16 + col) * L::ST1 + 4 * q;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                const f32x4 a = *reinterpret_cast<const f32x4 *>(arow + kb * 16);
+#pragma unroll
+                for (int j = 0; j < T; ++j)
+                    if (NT % 4 == 0 || wave + 4 * j < NT) acc[j][ct] = mfma4(f.v[j][kb], a, acc[j][ct]);
+            }
+        }
+        const bool last = s == p.n_steps - 1;
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            const int nt = wave + 4 * j;
+            if (NT % 4 != 0 && nt >= NT) continue;
+            const int n = nt * 16 + 4 * q;
+            const f32x4 b4 = ldg4(bias + n);
+#pragma unroll
+            for (int g = 0; g < (NB == 2 ? 1 : 2); ++g) {
+                // NB == 2: one candidate per lane column, eps_c = tile 0, eps_u = tile 1
+                // NB == 1: column tile g holds candidates 16g..16g+15
+                const int cl = NB == 2 ? col : g * 16 + col;
+                float *xp = lds + L::XB + (size_t)cl * L::SX + n;
+                const f32x4 x = *reinterpret_cast<const f32x4 *>(xp);
+                const f32x4 ec = acc[j][NB == 2 ? 0 : g] + b4;
+                const f32x4 eu = acc[j][1] + b4;
+                if (SMODE == MODE_EPS || SMODE == MODE_EPS1) {
+                    const int64_t gc = cand0 + cl;
+                    if (gc < p.batch) {
+                        *reinterpret_cast<f32x4 *>(p.x_out + (size_t)gc * D0 + n) = ec;
+                        if (SMODE == MODE_EPS) *reinterpret_cast<f32x4 *>(p.chain + (size_t)gc * D0 + n) = eu;
+                    }
+                    continue;
+                }
+                f32x4 xn;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float xv = x[r];
+                    float o;
+                    if (SMODE == MODE_DDPM_CFG) {
+                        const float x0c = sp.a * xv - sp.b * ec[r];
+                        const float x0u = sp.a * xv - sp.b * eu[r];
+                        float x0 = p.wp1 * x0c - p.wf * x0u;
+                        x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+                        const float mean = sp.c1 * x0 + sp.c2 * xv;
+                        o = (sp.flags & PLAN_NOISE) ? mean + sp.std * nz[j][0][r] : mean;
+                    } else if (SMODE == MODE_DDIM_CFG) {
+                        float x0 = p.wp1 * (sp.a * xv - sp.b * ec[r]) - p.wf * (sp.a * xv - sp.b * eu[r]);
+                        if (p.clamp_x0) x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+                        const float e = p.wp1 * ec[r] - p.wf * eu[r];
+                        o = (sp.flags & PLAN_FINAL) ? x0 : x0 * sp.sqan + sp.cn * e;
+                    } else {  // MODE_DDIM, 3-arg net
+                        float x0 = sp.a * xv - sp.b * ec[r];
+                        if (p.clamp_x0) x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+                        o = (sp.flags & PLAN_FINAL) ? x0 : x0 * sp.sqan + sp.cn * ec[r];
+                    }
+                    xn[r] = o;
+                }
+                *reinterpret_cast<f32x4 *>(xp) = xn;
+                const int64_t gc = cand0 + cl;
+                if (gc < p.batch) {
+                    if (p.chain)
+                        *reinterpret_cast<f32x4 *>(p.chain + ((size_t)(s + 1) * p.batch + gc) * D0 + n) = xn;
+                    if (last) *reinterpret_cast<f32x4 *>(p.x_out + (size_t)gc * D0 + n) = xn;
+                }
+            }
+        }
+    }
+
+    // noise of step s (slice s+1) for this lane's quads, fetched one step ahead of use
+    static MPCD_DEV void fetch_noise(f32x4 (&nz)[WFrag<32, D0, PAIRED>::T][NB], const MlpSampleArgs &p,
+                                     const StepPlan &sp, int s, int64_t cand0, int wave, int lane)
+    {
+        constexpr int T = WFrag<32, D0, PAIRED>::T, NT = D0 / 16;
+#pragma unroll
+        for (int j = 0; j < T; ++j)
+#pragma unroll
+            for (int g = 0; g < NB; ++g) nz[j][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (SMODE != MODE_DDPM_CFG || !(sp.flags & PLAN_NOISE)) return;  // DDIM: sigma = 0
+        const int col = lane & 15, q = lane >> 4;
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            const int nt = wave + 4 * j;
+            if (NT % 4 != 0 && nt >= NT) continue;
+            const int n = nt * 16 + 4 * q;
+            const int64_t gc = cand0 + col;  // DDPM-CFG only: NB == 2, one candidate per column
+            if (gc >= p.batch) continue;
+            if (p.noise)
+                nz[j][0] = *reinterpret_cast<const f32x4 *>(p.noise + ((size_t)(s + 1) * p.batch + gc) * D0 + n);
+            else
+                nz[j][0] = philox_normal4(p.seed, (uint64_t)(p.global_offset + gc), (uint32_t)(s + 1), (uint32_t)(n >> 2));
+        }
+    }
+
+    static MPCD_DEV void dump(const MlpSampleArgs &p, const float *buf, int stride, int width, int layer)
+    {
+        if (!p.dbg || blockIdx.x != 0) return;
+        lds_barrier();
+        for (int i = threadIdx.x; i < ROWS * width; i += THREADS) {
+            const int r = i / width, c = i - r * width;
+            p.dbg[(size_t)layer * ROWS * 256 + r * 256 + c] = buf[r * stride + c];
+        }
+    }
+
+    static MPCD_DEV void run(const MlpSampleArgs &p)
+    {
+        extern __shared__ float lds[];
+        const int lane = threadIdx.x & 63;
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const int64_t cand0 = (int64_t)blockIdx.x * CPW;
+        constexpr bool has_ctx = CTX;
+        const float *wp = p.wpack;
+        int wofs = 0;
+        auto W = [&](int l) { return wp + wofs + A::woff(l); };
+        auto Bs = [&](int l) { return wp + wofs + A::woff(l) + A::K[l] * A::N[l]; };
+
+        // per-candidate context projections (constant over the denoise loop)
+        if (has_ctx) {
+            for (int i = threadIdx.x; i < CPW * COND_TOTAL; i += THREADS) {
+                const int c = i / COND_TOTAL, k = i - c * COND_TOTAL;
+                const int64_t gc = cand0 + c;
+                lds[L::CP + i] = gc < p.batch ? p.cproj[(size_t)(p.cproj_stride ? gc : 0) * COND_TOTAL + k] : 0.f;
+            }
+        }
+        // x_T
+        for (int i = threadIdx.x; i < CPW * QUADS; i += THREADS) {
+            const int c = i / QUADS, qd = i - c * QUADS;
+            const int64_t gc = cand0 + c;
+            f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (gc < p.batch) {
+                z = p.noise ? *reinterpret_cast<const f32x4 *>(p.noise + (size_t)gc * D0 + qd * 4)
+                            : philox_normal4(p.seed, (uint64_t)(p.global_offset + gc), 0u, (uint32_t)qd);
+                if (p.chain && SMODE != MODE_EPS) *reinterpret_cast<f32x4 *>(p.chain + (size_t)gc * D0 + qd * 4) = z;
+            }
+            *reinterpret_cast<f32x4 *>(lds + L::XB + c * L::SX + qd * 4) = z;
+        }
+
+        WFrag<A::K[0], A::N[0], mode_for<A::N[0]>()> w0;
+        load_w(w0, W(0), wave, lane);
+        constexpr int NZT = WFrag<32, D0, PAIRED>::T;
+        f32x4 nz[NZT][NB];
+        StepPlan sp = p.plan[0];
+        fetch_noise(nz, p, sp, 0, cand0, wave, lane);
+
+        for (int s = 0; s < p.n_steps; ++s) {
+            // Launder the weight base every step: the weights are loop-invariant, and without this
+            // LICM hoists all 14 layers' loads out of the step loop (hundreds of live VGPRs -> spills).
+            asm volatile("" : "+s"(wofs));
+            WFrag<A::K[1], A::N[1], mode_for<A::N[1]>()> w1;
+            load_w(w1, W(1), wave, lane);
+            lds_barrier();
+            // this step's time projections -> LDS (first read by layer 1, after the next barrier)
+            for (int i = threadIdx.x; i < COND_TOTAL / 4; i += THREADS)
+                reinterpret_cast<f32x4 *>(lds + L::TP)[i] =
+                    reinterpret_cast<const f32x4 *>(p.tproj + (size_t)s * COND_TOTAL)[i];
+            const float *tp = lds + L::TP, *cp = lds + L::CP;
+            hidden_layer<A::K[0], A::N[0], mode_for<A::N[0]>(), EPI_MISH, NB>(w0, Bs(0), lds + L::XB, L::SX, NB == 2, lds + L::T1, L::ST1, tp,
+                                                         cp, 0, has_ctx, wave, lane);
+            dump(p, lds + L::T1, L::ST1, 32, 0);
+            WFrag<A::K[2], A::N[2], mode_for<A::N[2]>()> w2;
+            load_w(w2, W(2), wave, lane);
+            lds_barrier();
+            hidden_layer<A::K[1], A::N[1], mode_for<A::N[1]>(), EPI_CMISH, NB>(w1, Bs(1), lds + L::T1, L::ST1, false, lds + L::S1, L::SS1, tp, cp,
+                                                          0, has_ctx, wave, lane);
+            dump(p, lds + L::S1, L::SS1, 32, 1);
+            WFrag<A::K[3], A::N[3], mode_for<A::N[3]>()> w3;
+            load_w(w3, W(3), wave, lane);
+            lds_barrier();
+            hidden_layer<A::K[2], A::N[2], mode_for<A::N[2]>(), EPI_MISH, NB>(w2, Bs(2), lds + L::S1, L::SS1, false, lds + L::T1, L::ST1, tp, cp,
+                                                         0, has_ctx, wave, lane);
+            dump(p, lds + L::T1, L::ST1, 64, 2);
+            WFrag<A::K[4], A::N[4], mode_for<A::N[4]>()> w4;
+            load_w(w4, W(4), wave, lane);
+            lds_barrier();
+            hidden_layer<A::K[3], A::N[3], mode_for<A::N[3]>(), EPI_CMISH, NB>(w3, Bs(3), lds + L::T1, L::ST1, false, lds + L::C1 + 64, L::SC1,
+                                                          tp, cp, 1, has_ctx, wave, lane);
+            dump(p, lds + L::C1 + 64, L::SC1, 64, 3);
+            WFrag<A::K[5], A::N[5], mode_for<A::N[5]>()> w5;
+            load_w(w5, W(5), wave, lane);
+            lds_barrier();
+            hidden_layer<A::K[4], A::N[4], mode_for<A::N[4]>(), EPI_MISH, NB>(w4, Bs(4), lds + L::C1 + 64, L::SC1, false, lds + L::T1, L::ST1,
+                                                         tp, cp, 0, has_ctx, wave, lane);
+            dump(p, lds + L::T1, L::ST1, 128, 4);
+            WFrag<A::K[6], A::N[6], mode_for<A::N[6]>()> w6;
+            load_w(w6, W(6), wave, lane);
+            lds_barrier();
+            hidden_layer<A::K[5], A::N[5], mode_for<A::N[5]>(), EPI_CMISH, NB>(w5, Bs(5), lds + L::T1, L::ST1, false, lds + L::C0 + 128,
+                                                          L::SC0, tp, cp, 2, has_ctx, wave, lane);
+            dump(p, lds + L::C0 + 128, L::SC0, 128, 5);
+            WFrag<A::K[7], A::N[7], mode_for<A::N[7]>()> w7;
+            load_w(w7, W(7), wave, lane);
+            lds_barrier();
+            hidden_layer<A::K[6], A::N[6], mode_for<A::N[6]>(), EPI_MISH, NB>(w6, Bs(6), lds + L::C0 + 128, L::SC0, false, lds + L::T1, L::ST1,
+                                                         tp, cp, 0, has_ctx, wave, lane);
+            dump(p, lds + L::T1, L::ST1, 128, 6);
+            WFrag<A::K[8], A::N[8], mode_for<A::N[8]>()> w8;
+            load_w(w8, W(8), wave, lane);
+            lds_barrier();
+            hidden_layer<A::K[7], A::N[7], mode_for<A::N[7]>(), EPI_CMISH, NB>(w7, Bs(7), lds + L::T1, L::ST1, false, lds + L::C0, L::SC0, tp,
+                                                          cp, 3, has_ctx, wave, lane);
+            dump(p, lds + L::C0, L::SC0, 128, 7);
+            WFrag<A::K[9], A::N[9], mode_for<A::N[9]>()> w9;
+            load_w(w9, W(9), wave, lane);
+            lds_barrier();
+            hidden_layer<A::K[8], A::N[8], mode_for<A::N[8]>(), EPI_MISH, NB>(w8, Bs(8), lds + L::C0, L::SC0, false, lds + L::T1, L::ST1, tp, cp,
+                                                         0, has_ctx, wave, lane);
+            dump(p, lds + L::T1, L::ST1, 64, 8);
+            WFrag<A::K[10], A::N[10], mode_for<A::N[10]>()> w10;
+            load_w(w10, W(10), wave, lane);
+            lds_barrier();
+            hidden_layer<A::K[9], A::N[9], mode_for<A::N[9]>(), EPI_CMISH, NB>(w9, Bs(9), lds + L::T1, L::ST1, false, lds + L::C1, L::SC1, tp,
+                                                          cp, 4, has_ctx, wave, lane);
+            dump(p, lds + L::C1, L::SC1, 64, 9);
+            WFrag<A::K[11], A::N[11], mode_for<A::N[11]>()> w11;
+            load_w(w11, W(11), wave, lane);
+            lds_barrier();
+            hidden_layer<A::K[10], A::N[10], mode_for<A::N[10]>(), EPI_MISH, NB>(w10, Bs(10), lds + L::C1, L::SC1, false, lds + L::T1, L::ST1,
+                                                           tp, cp, 0, has_ctx, wave, lane);
+            dump(p, lds + L::T1, L::ST1, 32, 10);
+            WFrag<A::K[12], A::N[12], mode_for<A::N[12]>()> w12;
+            load_w(w12, W(12), wave, lane);
+            lds_barrier();
+            hidden_layer<A::K[11], A::N[11], mode_for<A::N[11]>(), EPI_CMISH, NB>(w11, Bs(11), lds + L::T1, L::ST1, false, lds + L::S1, L::SS1,
+                                                            tp, cp, 5, has_ctx, wave, lane);
+            dump(p, lds + L::S1, L::SS1, 32, 11);
+            WFrag<A::K[13], A::N[13], PAIRED> w13;
+            load_w(w13, W(13), wave, lane);
+            lds_barrier();
+            hidden_layer<A::K[12], A::N[12], mode_for<A::N[12]>(), EPI_NONE, NB>(w12, Bs(12), lds + L::S1, L::SS1, false, lds + L::T1, L::ST1,
+                                                           tp, cp, 0, has_ctx, wave, lane);
+            dump(p, lds + L::T1, L::ST1, 32, 12);
+            if (s + 1 < p.n_steps) load_w(w0, W(0), wave, lane);
+            const StepPlan cur = sp;
+            f32x4 nzc[NZT][NB];
+#pragma unroll
+            for (int j = 0; j < NZT; ++j)
+#pragma unroll
+                for (int g = 0; g < NB; ++g) nzc[j][g] = nz[j][g];
+            if (s + 1 < p.n_steps) {
+                sp = p.plan[s + 1];
+                fetch_noise(nz, p, sp, s + 1, cand0, wave, lane);
+            }
+            lds_barrier();
+            final_and_update(w13, Bs(13), lds, p, cur, s, cand0, nzc, wave, lane);
+        }
+    }
+};
+
+template <int D0, int SMODE, bool CTX>
+__global__ __launch_bounds__(THREADS, 1) void mlp_sample_kernel(const MlpSampleArgs p)
+{
+    MlpKernel<D0, SMODE, CTX>::run(p);
+}
+
+template <int D0, int SMODE, bool CTX>
+hipError_t launch_impl(const MlpSampleArgs &a, hipStream_t stream)
+{
+    using L = Lds<D0, MlpKernel<D0, SMODE, CTX>::NB>;
+    const size_t lds_bytes = sizeof(float) * L::total(CTX);
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&mlp_sample_kernel<D0, SMODE, CTX>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    const int64_t blocks = (a.batch + L::CPW - 1) / L::CPW;
+    hipLaunchKernelGGL((mlp_sample_kernel<D0, SMODE, CTX>), dim3((unsigned)blocks), dim3(THREADS), lds_bytes, stream, a);
+    return hipGetLastError();
+}
+
+template <int D0>
+hipError_t launch_d0(const MlpSampleArgs &a, hipStream_t stream)
+{
+    const bool ctx = a.cproj != nullptr;
+    switch (a.mode) {
+    case MODE_DDPM_CFG: return ctx ? launch_impl<D0, MODE_DDPM_CFG, true>(a, stream) : launch_impl<D0, MODE_DDPM_CFG, false>(a, stream);
+    case MODE_DDIM_CFG: return ctx ? launch_impl<D0, MODE_DDIM_CFG, true>(a, stream) : launch_impl<D0, MODE_DDIM_CFG, false>(a, stream);
+    case MODE_DDIM: return ctx ? launch_impl<D0, MODE_DDIM, true>(a, stream) : launch_impl<D0, MODE_DDIM, false>(a, stream);
+    case MODE_EPS: return ctx ? launch_impl<D0, MODE_EPS, true>(a, stream) : launch_impl<D0, MODE_EPS, false>(a, stream);
+    case MODE_EPS1: return ctx ? launch_impl<D0, MODE_EPS1, true>(a, stream) : launch_impl<D0, MODE_EPS1, false>(a, stream);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+int mlp_packed_floats(int d0)
+{
+    switch (d0) {
+    case 32: return Arch<32>::total();
+    case 64: return Arch<64>::total();
+    case 128: return Arch<128>::total();
+    default: return -1;
+    }
+}
+
+// Pack Linear l (torch weight [N][K], bias [N]) to the MFMA A-operand order:
+// packed[((nt*KB + kb)*64 + lane)*4 + s] = W[nt*16 + (lane&15)][kb*16 + 4*(lane>>4) + s], then bias.
+void mlp_pack_weights(int d0, const float *const *lin_w, const float *const *lin_b, float *out)
+{
+    const int Ks[NLAYER] = {d0, 32, 32, 64, 64, 128, 128, 128, 256, 64, 128, 32, 32, 32};
+    const int Ns[NLAYER] = {32, 32, 64, 64, 128, 128, 128, 128, 64, 64, 32, 32, 32, d0};
+    size_t o = 0;
+    for (int l = 0; l < NLAYER; ++l) {
+        const int K = Ks[l], N = Ns[l], KB = K / 16, NT = N / 16;
+        for (int nt = 0; nt < NT; ++nt)
+            for (int kb = 0; kb < KB; ++kb)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int s = 0; s < 4; ++s)
+                        out[o + (((size_t)nt * KB + kb) * 64 + lane) * 4 + s] =
+                            lin_w[l][(size_t)(nt * 16 + (lane & 15)) * K + kb * 16 + 4 * (lane >> 4) + s];
+        o += (size_t)K * N;
+        for (int n = 0; n < N; ++n) out[o + n] = lin_b[l][n];
+        o += N;
+    }
+}
+
+hipError_t launch_mlp_sampler(int d0, int nb, const MlpSampleArgs &a, hipStream_t stream)
+{
+    if ((nb == 1) != (a.mode == MODE_DDIM || a.mode == MODE_EPS1)) return hipErrorInvalidValue;
+    switch (d0) {
+    case 32: return launch_d0<32>(a, stream);
+    case 64: return launch_d0<64>(a, stream);
+    case 128: return launch_d0<128>(a, stream);
+    }
+    return hipErrorInvalidValue;
+}

@@ -1,0 +1,697 @@
+// C ABI of libmpcd.so (include/mpcd.h): context, weight repacking, schedule -> step plans, and the
+// host side of every launch. Host-only code; the kernels live in mlp_sampler.hip,
+// cond_prologue.hip, rollout.hip and unet.hip.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/mpcd.h"
+#include "internal.h"
+#include "unet.h"
+
+hipError_t launch_clip_flag(const float *x, int64_t n, int *flag_dev, hipStream_t stream);
+hipError_t launch_unnormalize(const float *x, int64_t n, int dim, const int *flag_dev, const float *mn_host,
+                              const float *mx_host, float *out, hipStream_t stream);
+hipError_t launch_rollout_cost(const mpcd_system_desc &d, const double *x0_host, const float *u_norm,
+                               const float *umin_host, const float *umax_host, const int *flag_dev, int64_t batch, int H,
+                               double *cost, hipStream_t stream);
+hipError_t launch_argmin(const double *cost, int64_t n, int64_t offset, mpcd_best *best, hipStream_t stream);
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) return fail(MPCD_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+struct PSpec {
+    std::string name;
+    std::vector<int64_t> shape;
+    int64_t numel() const
+    {
+        int64_t n = 1;
+        for (auto s : shape) n *= s;
+        return n;
+    }
+};
+
+int cond_dim_of(const mpcd_net_desc &d) { return d.time_emb_dim + d.context_dim; }
+
+void add(std::vector<PSpec> &v, const std::string &n, std::vector<int64_t> s) { v.push_back({n, std::move(s)}); }
+
+void time_mlp_spec(std::vector<PSpec> &v, const mpcd_net_desc &d)
+{
+    add(v, "time_mlp.encoder.1.weight", {128, 32});
+    add(v, "time_mlp.encoder.1.bias", {128});
+    add(v, "time_mlp.encoder.3.weight", {d.time_emb_dim, 128});
+    add(v, "time_mlp.encoder.3.bias", {d.time_emb_dim});
+}
+
+// TemporalBlockMLP (layers.py:358-385)
+void tbm_spec(std::vector<PSpec> &v, const std::string &p, int ci, int co, int cond)
+{
+    add(v, p + ".blocks.0._network.0.weight", {co, ci});
+    add(v, p + ".blocks.0._network.0.bias", {co});
+    add(v, p + ".blocks.0._network.2.weight", {co, co});
+    add(v, p + ".blocks.0._network.2.bias", {co});
+    add(v, p + ".cond_mlp.1.weight", {co, cond});
+    add(v, p + ".cond_mlp.1.bias", {co});
+}
+
+// ResidualTemporalBlock (layers.py:323-355)
+void rtb_spec(std::vector<PSpec> &v, const std::string &p, int ci, int co, int cond)
+{
+    add(v, p + ".blocks.0.block.0.weight", {co, ci, 5});
+    add(v, p + ".blocks.0.block.0.bias", {co});
+    add(v, p + ".blocks.0.block.2.weight", {co});
+    add(v, p + ".blocks.0.block.2.bias", {co});
+    add(v, p + ".blocks.1.block.0.weight", {co, co, 5});
+    add(v, p + ".blocks.1.block.0.bias", {co});
+    add(v, p + ".blocks.1.block.2.weight", {co});
+    add(v, p + ".blocks.1.block.2.bias", {co});
+    add(v, p + ".cond_mlp.1.weight", {co, cond});
+    add(v, p + ".cond_mlp.1.bias", {co});
+    if (ci != co) {
+        add(v, p + ".residual_conv.weight", {co, ci, 1});
+        add(v, p + ".residual_conv.bias", {co});
+    }
+}
+
+std::vector<std::pair<int, int>> stages(int first, const mpcd_net_desc &d)
+{
+    std::vector<std::pair<int, int>> s;
+    int prev = first;
+    for (int i = 0; i < d.n_mults; ++i) {
+        s.push_back({prev, d.base_dim * d.mults[i]});
+        prev = d.base_dim * d.mults[i];
+    }
+    return s;
+}
+
+// state_dict() order of the torch module (registration order: time_mlp, downs, ups, mid, final)
+std::vector<PSpec> param_spec(const mpcd_net_desc &d)
+{
+    std::vector<PSpec> v;
+    const int cond = cond_dim_of(d);
+    time_mlp_spec(v, d);
+    if (d.kind == MPCD_NET_MLP) {
+        const int flat = d.horizon * d.state_dim;
+        auto st = stages(flat, d);
+        for (size_t i = 0; i < st.size(); ++i) tbm_spec(v, "downs." + std::to_string(i) + ".0", st[i].first, st[i].second, cond);
+        for (size_t i = 1; i < st.size(); ++i) {
+            auto [ci, co] = st[st.size() - i];
+            tbm_spec(v, "ups." + std::to_string(i - 1) + ".0", 2 * co, ci, cond);
+        }
+        const int mid = st.back().second;
+        tbm_spec(v, "mid_block1", mid, mid, cond);
+        add(v, "final_layer.0._network.0.weight", {d.base_dim, d.base_dim});
+        add(v, "final_layer.0._network.0.bias", {d.base_dim});
+        add(v, "final_layer.0._network.2.weight", {flat, d.base_dim});
+        add(v, "final_layer.0._network.2.bias", {flat});
+    } else {
+        auto st = stages(d.state_dim, d);
+        const int nres = (int)st.size();
+        for (int i = 0; i < nres; ++i) {
+            const std::string p = "downs." + std::to_string(i);
+            rtb_spec(v, p + ".0", st[i].first, st[i].second, cond);
+            rtb_spec(v, p + ".1", st[i].second, st[i].second, cond);
+            if (i < nres - 1) {
+                add(v, p + ".4.conv.weight", {st[i].second, st[i].second, 3});
+                add(v, p + ".4.conv.bias", {st[i].second});
+            }
+        }
+        for (int i = 1; i < nres; ++i) {
+            auto [ci, co] = st[nres - i];
+            const std::string p = "ups." + std::to_string(i - 1);
+            rtb_spec(v, p + ".0", 2 * co, ci, cond);
+            rtb_spec(v, p + ".1", ci, ci, cond);
+            add(v, p + ".4.conv.weight", {ci, ci, 4});
+            add(v, p + ".4.conv.bias", {ci});
+        }
+        const int mid = st.back().second;
+        rtb_spec(v, "mid_block1", mid, mid, cond);
+        rtb_spec(v, "mid_block2", mid, mid, cond);
+        add(v, "final_conv.0.block.0.weight", {d.base_dim, d.base_dim, 5});
+        add(v, "final_conv.0.block.0.bias", {d.base_dim});
+        add(v, "final_conv.0.block.2.weight", {d.base_dim});
+        add(v, "final_conv.0.block.2.bias", {d.base_dim});
+        add(v, "final_conv.1.weight", {d.state_dim, d.base_dim, 1});
+        add(v, "final_conv.1.bias", {d.state_dim});
+    }
+    return v;
+}
+
+int check_desc(const mpcd_net_desc *d)
+{
+    if (!d) return fail(MPCD_EINVAL, "null desc");
+    if (d->kind != MPCD_NET_MLP && d->kind != MPCD_NET_UNET) return fail(MPCD_EINVAL, "bad net kind %d", d->kind);
+    if (d->state_dim < 1 || d->horizon < 1 || d->context_dim < 0 || d->base_dim < 1 || d->n_mults < 1 ||
+        d->n_mults > 4 || d->time_emb_dim != 32)
+        return fail(MPCD_EINVAL, "bad net dims");
+    for (int i = 0; i < d->n_mults; ++i)
+        if (d->mults[i] < 1) return fail(MPCD_EINVAL, "bad dim_mults");
+    return MPCD_OK;
+}
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t n)
+    {
+        if (n <= bytes) return MPCD_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (hipMalloc(&p, n) != hipSuccess) return fail(MPCD_ENOMEM, "hipMalloc(%zu) failed", n);
+        bytes = n;
+        return MPCD_OK;
+    }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+}  // namespace
+
+struct mpcd_ctx {
+    int device = 0;
+    bool net_loaded = false;
+    mpcd_net_desc desc{};
+    int cond_dim = 0, cond_total = 0, n_cond = 0;
+    DevBuf params;      // raw blob (time MLP, cond layers, UNet tensors)
+    DevBuf wpack;       // MLP packed linear layers
+    DevBuf cond_layers; // CondLayer[n_cond]
+    UnetWeights unet{}; // device pointers into `params` + repacked conv weights
+    DevBuf unet_pack;
+    // schedule
+    std::vector<float> tables;  // 12 x N
+    std::vector<float> post_std;
+    int n_steps = 0;
+    // workspace
+    DevBuf plan, tproj, cproj, flag, unet_ws;
+    std::vector<StepPlan> plan_host;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    float *dbg = nullptr;  // debug dump target for mpcd_eps (mpcd_debug_set)
+};
+
+namespace {
+
+enum {
+    T_BETAS = 0, T_AC, T_ACP, T_SQAC, T_SQ1MAC, T_LOG1MAC, T_SRAC, T_SRM1AC, T_PV, T_PLVC, T_C1, T_C2
+};
+
+float tab(const mpcd_ctx *c, int which, int t) { return c->tables[(size_t)which * c->n_steps + t]; }
+
+// Build the per-step plan (sample_functions.py:28-44 for DDPM; diffusion_model_base.py:251-290 for DDIM).
+int build_plan(mpcd_ctx *c, const mpcd_sample_args *a, std::vector<StepPlan> &plan)
+{
+    plan.clear();
+    const int N = c->n_steps;
+    if (a->sampler == MPCD_DDPM_CFG) {
+        if (a->n_wo_noise < 0) return fail(MPCD_EINVAL, "n_wo_noise < 0");
+        for (int i = N - 1; i >= -a->n_wo_noise; --i) {
+            const int t = i < 0 ? 0 : i;
+            StepPlan s{};
+            s.t = t;
+            s.flags = t > 0 ? PLAN_NOISE : 0;
+            s.a = tab(c, T_SRAC, t);
+            s.b = tab(c, T_SRM1AC, t);
+            s.c1 = tab(c, T_C1, t);
+            s.c2 = tab(c, T_C2, t);
+            s.std = c->post_std[t];
+            plan.push_back(s);
+        }
+        return MPCD_OK;
+    }
+    // DDIM: times = reversed(int(cat([-1], linspace(0, N-1, S+1)))) unless given explicitly
+    std::vector<int> times;
+    if (a->ddim_times && a->n_ddim_times > 1) {
+        times.assign(a->ddim_times, a->ddim_times + a->n_ddim_times);
+    } else {
+        const int S = a->ddim_steps > 0 ? a->ddim_steps : N / 5;
+        if (S < 1) return fail(MPCD_EINVAL, "DDIM needs at least one sampling step");
+        // torch.linspace (fp32, scalar path): start + step*i for i < steps/2, else end - step*(steps-1-i)
+        const int steps = S + 1;
+        const float start = 0.f, end = (float)(N - 1);
+        const float stp = (end - start) / (float)(steps - 1);
+        std::vector<int> g;
+        for (int i = 0; i < steps; ++i) {
+            const float v = i < steps / 2 ? start + stp * (float)i : end - stp * (float)(steps - i - 1);
+            g.push_back((int)v);
+        }
+        times.push_back(-1);
+        times.insert(times.end(), g.begin(), g.end());
+        std::reverse(times.begin(), times.end());
+    }
+    for (size_t k = 0; k + 1 < times.size(); ++k) {
+        const int t = times[k], tn = times[k + 1];
+        if (t < 0 || t >= N || tn >= N) return fail(MPCD_EINVAL, "DDIM time out of range");
+        StepPlan s{};
+        s.t = t;
+        s.a = tab(c, T_SRAC, t);
+        s.b = tab(c, T_SRM1AC, t);
+        if (tn < 0) {
+            s.flags = PLAN_FINAL;
+            plan.push_back(s);
+            break;
+        }
+        const float an = tab(c, T_AC, tn);
+        s.sqan = sqrtf(an);
+        s.cn = sqrtf(1.0f - an - 0.0f);  // sigma = eta * (...) = 0 (eta = 0, :253)
+        plan.push_back(s);
+    }
+    return MPCD_OK;
+}
+
+int upload_net(mpcd_ctx *c, const mpcd_net_desc &d, const float *blob, size_t n_floats)
+{
+    auto spec = param_spec(d);
+    size_t total = 0;
+    for (auto &p : spec) total += (size_t)p.numel();
+    if (n_floats != total) return fail(MPCD_EINVAL, "blob has %zu floats, net needs %zu", n_floats, total);
+    std::vector<size_t> off;
+    size_t o = 0;
+    for (auto &p : spec) {
+        off.push_back(o);
+        o += (size_t)p.numel();
+    }
+    auto find = [&](const std::string &n) -> int {
+        for (size_t i = 0; i < spec.size(); ++i)
+            if (spec[i].name == n) return (int)i;
+        return -1;
+    };
+    int rc = c->params.ensure(total * sizeof(float));
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(c->params.p, blob, total * sizeof(float), hipMemcpyHostToDevice));
+    const float *dbase = c->params.as<float>();
+    auto dptr = [&](const std::string &n) { return dbase + off[find(n)]; };
+
+    // conditioning layers: every "*.cond_mlp.1.weight" in spec order
+    std::vector<CondLayer> cl;
+    int cond_total = 0;
+    for (size_t i = 0; i < spec.size(); ++i) {
+        const std::string &n = spec[i].name;
+        const std::string suf = ".cond_mlp.1.weight";
+        if (n.size() > suf.size() && n.compare(n.size() - suf.size(), suf.size(), suf) == 0) {
+            CondLayer L;
+            L.W = dbase + off[i];
+            L.b = dbase + off[i + 1];
+            L.width = (int)spec[i].shape[0];
+            L.off = cond_total;
+            cond_total += L.width;
+            cl.push_back(L);
+        }
+    }
+    if (d.kind == MPCD_NET_MLP) {
+        // MLP kernel consumes cond blocks in execution order: downs 0..2, mid, ups 0..1
+        // (spec order is downs, ups, mid) -> reorder to execution order and fixed offsets.
+        if (cl.size() != 6) return fail(MPCD_EUNSUP, "MLP needs dim_mults of length 3");
+        std::vector<CondLayer> ex = {cl[0], cl[1], cl[2], cl[5], cl[3], cl[4]};
+        int ofs = 0;
+        for (auto &L : ex) {
+            L.off = ofs;
+            ofs += L.width;
+        }
+        cl = ex;
+        const int d0 = d.horizon * d.state_dim;
+        if (d.base_dim != 32 || d.mults[0] != 1 || d.mults[1] != 2 || d.mults[2] != 4 || mlp_packed_floats(d0) < 0)
+            return fail(MPCD_EUNSUP, "MLP kernel supports base 32, mults (1,2,4), H*d in {32,64,128}");
+        // gather the 14 Linear layers in execution order
+        const char *names[14] = {"downs.0.0.blocks.0._network.0", "downs.0.0.blocks.0._network.2",
+                                 "downs.1.0.blocks.0._network.0", "downs.1.0.blocks.0._network.2",
+                                 "downs.2.0.blocks.0._network.0", "downs.2.0.blocks.0._network.2",
+                                 "mid_block1.blocks.0._network.0", "mid_block1.blocks.0._network.2",
+                                 "ups.0.0.blocks.0._network.0", "ups.0.0.blocks.0._network.2",
+                                 "ups.1.0.blocks.0._network.0", "ups.1.0.blocks.0._network.2",
+                                 "final_layer.0._network.0", "final_layer.0._network.2"};
+        const float *lw[14], *lb[14];
+        for (int l = 0; l < 14; ++l) {
+            const int iw = find(std::string(names[l]) + ".weight"), ib = find(std::string(names[l]) + ".bias");
+            if (iw < 0 || ib < 0) return fail(MPCD_EINVAL, "missing %s", names[l]);
+            lw[l] = blob + off[iw];
+            lb[l] = blob + off[ib];
+        }
+        std::vector<float> packed((size_t)mlp_packed_floats(d0));
+        mlp_pack_weights(d0, lw, lb, packed.data());
+        rc = c->wpack.ensure(packed.size() * sizeof(float));
+        if (rc) return rc;
+        HIP_TRY(hipMemcpy(c->wpack.p, packed.data(), packed.size() * sizeof(float), hipMemcpyHostToDevice));
+    } else {
+        rc = unet_prepare(d, spec.size(), [&](const char *n) -> const float * {
+            const int i = find(n);
+            return i < 0 ? nullptr : dbase + off[i];
+        }, [&](const char *n) -> const float * {
+            const int i = find(n);
+            return i < 0 ? nullptr : blob + off[i];
+        }, c->unet, c->unet_pack.p, c->unet_pack.bytes);
+        if (rc) return fail(rc, "unet_prepare: %s", unet_last_error());
+    }
+    rc = c->cond_layers.ensure(cl.size() * sizeof(CondLayer));
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(c->cond_layers.p, cl.data(), cl.size() * sizeof(CondLayer), hipMemcpyHostToDevice));
+    c->n_cond = (int)cl.size();
+    c->cond_total = cond_total;
+    c->cond_dim = cond_dim_of(d);
+    c->desc = d;
+    c->net_loaded = true;
+    return MPCD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *mpcd_last_error(void) { return g_err.c_str(); }
+
+int mpcd_net_param_count(const mpcd_net_desc *desc, int32_t *n_tensors, int64_t *n_floats)
+{
+    int rc = check_desc(desc);
+    if (rc) return rc;
+    auto spec = param_spec(*desc);
+    int64_t n = 0;
+    for (auto &p : spec) n += p.numel();
+    if (n_tensors) *n_tensors = (int32_t)spec.size();
+    if (n_floats) *n_floats = n;
+    return MPCD_OK;
+}
+
+int mpcd_net_param_info(const mpcd_net_desc *desc, int32_t i, char *name, size_t name_cap, int32_t *ndim,
+                        int64_t shape[4])
+{
+    int rc = check_desc(desc);
+    if (rc) return rc;
+    auto spec = param_spec(*desc);
+    if (i < 0 || i >= (int32_t)spec.size()) return fail(MPCD_EINVAL, "tensor index %d out of range", i);
+    const PSpec &p = spec[i];
+    if (name && name_cap) snprintf(name, name_cap, "%s", p.name.c_str());
+    if (ndim) *ndim = (int32_t)p.shape.size();
+    if (shape)
+        for (size_t k = 0; k < 4; ++k) shape[k] = k < p.shape.size() ? p.shape[k] : 1;
+    return MPCD_OK;
+}
+
+int mpcd_create(int device, mpcd_ctx **out)
+{
+    if (!out) return fail(MPCD_EINVAL, "null out");
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail(MPCD_EINVAL, "device %d of %d", device, n);
+    HIP_TRY(hipSetDevice(device));
+    auto *c = new mpcd_ctx();
+    c->device = device;
+    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        delete c;
+        return fail(MPCD_EHIP, "hipEventCreate failed");
+    }
+    if (int rc = c->flag.ensure(64)) {
+        delete c;
+        return rc;
+    }
+    *out = c;
+    return MPCD_OK;
+}
+
+void mpcd_destroy(mpcd_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    for (DevBuf *b : {&c->params, &c->wpack, &c->cond_layers, &c->unet_pack, &c->plan, &c->tproj, &c->cproj, &c->flag,
+                      &c->unet_ws})
+        b->release();
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    delete c;
+}
+
+int mpcd_load_net(mpcd_ctx *c, const mpcd_net_desc *desc, const float *blob, size_t n_floats)
+{
+    if (!c || !blob) return fail(MPCD_EINVAL, "null argument");
+    int rc = check_desc(desc);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    c->net_loaded = false;
+    return upload_net(c, *desc, blob, n_floats);
+}
+
+int mpcd_set_schedule(mpcd_ctx *c, const float *tables, int32_t n_steps, const float *post_std)
+{
+    if (!c || !tables || n_steps < 1) return fail(MPCD_EINVAL, "bad schedule arguments");
+    c->tables.assign(tables, tables + (size_t)12 * n_steps);
+    c->post_std.resize(n_steps);
+    for (int t = 0; t < n_steps; ++t)
+        c->post_std[t] = post_std ? post_std[t] : sqrtf(expf(tables[(size_t)T_PLVC * n_steps + t]));
+    c->n_steps = n_steps;
+    return MPCD_OK;
+}
+
+int mpcd_sample_steps(mpcd_ctx *c, const mpcd_sample_args *a, int32_t *n)
+{
+    if (!c || !a || !n) return fail(MPCD_EINVAL, "null argument");
+    if (!c->n_steps) return fail(MPCD_ESTATE, "no schedule set");
+    std::vector<StepPlan> plan;
+    int rc = build_plan(c, a, plan);
+    if (rc) return rc;
+    *n = (int32_t)plan.size();
+    return MPCD_OK;
+}
+
+int mpcd_sample(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr)
+{
+    if (!c || !a) return fail(MPCD_EINVAL, "null argument");
+    if (!c->net_loaded) return fail(MPCD_ESTATE, "no net loaded");
+    if (!c->n_steps) return fail(MPCD_ESTATE, "no schedule set");
+    if (!a->x_out || a->batch < 1) return fail(MPCD_EINVAL, "x_out / batch");
+    const mpcd_net_desc &d = c->desc;
+    const bool cfg = a->sampler == MPCD_DDPM_CFG || a->sampler == MPCD_DDIM_CFG;
+    if (a->sampler < 0 || a->sampler > MPCD_DDIM) return fail(MPCD_EINVAL, "bad sampler %d", a->sampler);
+    if (cfg != (d.cfg_masked != 0)) return fail(MPCD_EINVAL, "CFG samplers need a cfg_masked net and vice versa");
+    if (d.context_dim > 0 && !a->context) return fail(MPCD_EINVAL, "net has a context but none given");
+    hipStream_t st = static_cast<hipStream_t>(stream_ptr);
+    HIP_TRY(hipSetDevice(c->device));
+
+    int rc = build_plan(c, a, c->plan_host);
+    if (rc) return rc;
+    const int S = (int)c->plan_host.size();
+    if ((rc = c->plan.ensure(sizeof(StepPlan) * S))) return rc;
+    HIP_TRY(hipMemcpyAsync(c->plan.p, c->plan_host.data(), sizeof(StepPlan) * S, hipMemcpyHostToDevice, st));
+    if ((rc = c->tproj.ensure(sizeof(float) * (size_t)S * c->cond_total))) return rc;
+    const CondLayer *cl = c->cond_layers.as<CondLayer>();
+    const float *P = c->params.as<float>();
+    // time MLP = the first four tensors of the blob
+    const float *tw1 = P, *tb1 = tw1 + 128 * 32, *tw2 = tb1 + 128, *tb2 = tw2 + 32 * 128;
+    launch_time_prologue(c->plan.as<StepPlan>(), S, tw1, tb1, tw2, tb2, cl, c->n_cond, c->cond_dim, c->cond_total,
+                         c->tproj.as<float>(), st);
+    HIP_TRY(hipGetLastError());
+    const float *cproj = nullptr;
+    int64_t cstride = 0;
+    if (d.context_dim > 0) {
+        const int64_t rows = a->context_shared ? 1 : a->batch;
+        if ((rc = c->cproj.ensure(sizeof(float) * (size_t)rows * c->cond_total))) return rc;
+        launch_ctx_prologue(a->context, rows, d.context_dim, cl, c->n_cond, c->cond_dim, c->cond_total,
+                            c->cproj.as<float>(), st);
+        HIP_TRY(hipGetLastError());
+        cproj = c->cproj.as<float>();
+        cstride = a->context_shared ? 0 : c->cond_total;
+    }
+    const float wp1 = (float)(1.0 + a->w), wf = (float)a->w;
+    HIP_TRY(hipEventRecord(c->ev0, st));
+    if (d.kind == MPCD_NET_MLP) {
+        MlpSampleArgs m{};
+        m.wpack = c->wpack.as<float>();
+        m.plan = c->plan.as<StepPlan>();
+        m.tproj = c->tproj.as<float>();
+        m.cproj = cproj;
+        m.cproj_stride = cstride;
+        m.noise = a->noise;
+        m.x_out = a->x_out;
+        m.chain = a->chain_out;
+        m.batch = a->batch;
+        m.global_offset = a->global_offset;
+        m.seed = a->seed;
+        m.n_steps = S;
+        m.mode = a->sampler;
+        m.clamp_x0 = a->clamp_x0;
+        m.wp1 = wp1;
+        m.wf = wf;
+        HIP_TRY(launch_mlp_sampler(d.horizon * d.state_dim, cfg ? 2 : 1, m, st));
+    } else {
+        UnetSampleArgs u{};
+        u.plan = c->plan.as<StepPlan>();
+        u.plan_host = c->plan_host.data();
+        u.tproj = c->tproj.as<float>();
+        u.cproj = cproj;
+        u.cproj_stride = cstride;
+        u.cond_total = c->cond_total;
+        u.noise = a->noise;
+        u.x_out = a->x_out;
+        u.chain = a->chain_out;
+        u.batch = a->batch;
+        u.global_offset = a->global_offset;
+        u.seed = a->seed;
+        u.n_steps = S;
+        u.mode = a->sampler;
+        u.clamp_x0 = a->clamp_x0;
+        u.wp1 = wp1;
+        u.wf = wf;
+        size_t ws = unet_workspace_bytes(d, a->batch, cfg ? 2 : 1);
+        if ((rc = c->unet_ws.ensure(ws))) return rc;
+        u.workspace = c->unet_ws.p;
+        rc = unet_sample(d, c->unet, u, st);
+        if (rc) return fail(rc, "unet_sample: %s", unet_last_error());
+    }
+    HIP_TRY(hipEventRecord(c->ev1, st));
+    c->timed = true;
+    return MPCD_OK;
+}
+
+int mpcd_eps(mpcd_ctx *c, const float *x, int32_t t, const float *context, int32_t context_shared, int64_t batch,
+             float *eps_cond, float *eps_uncond, void *stream_ptr)
+{
+    if (!c || !x || !eps_cond || batch < 1) return fail(MPCD_EINVAL, "bad mpcd_eps arguments");
+    if (!c->net_loaded) return fail(MPCD_ESTATE, "no net loaded");
+    if (!c->n_steps) return fail(MPCD_ESTATE, "no schedule set");
+    const mpcd_net_desc &d = c->desc;
+    const bool cfg = d.cfg_masked != 0;
+    if (cfg && !eps_uncond) return fail(MPCD_EINVAL, "cfg net needs eps_uncond");
+    if (d.context_dim > 0 && !context) return fail(MPCD_EINVAL, "net has a context but none given");
+    if (t < 0 || t >= c->n_steps) return fail(MPCD_EINVAL, "t out of range");
+    if (d.kind != MPCD_NET_MLP) return fail(MPCD_EUNSUP, "mpcd_eps: UNet forward goes through unet_eps");
+    hipStream_t st = static_cast<hipStream_t>(stream_ptr);
+    HIP_TRY(hipSetDevice(c->device));
+    StepPlan sp{};
+    sp.t = t;
+    c->plan_host.assign(1, sp);
+    int rc;
+    if ((rc = c->plan.ensure(sizeof(StepPlan)))) return rc;
+    HIP_TRY(hipMemcpyAsync(c->plan.p, c->plan_host.data(), sizeof(StepPlan), hipMemcpyHostToDevice, st));
+    if ((rc = c->tproj.ensure(sizeof(float) * (size_t)c->cond_total))) return rc;
+    const CondLayer *cl = c->cond_layers.as<CondLayer>();
+    const float *P = c->params.as<float>();
+    launch_time_prologue(c->plan.as<StepPlan>(), 1, P, P + 128 * 32, P + 128 * 32 + 128, P + 128 * 32 + 128 + 32 * 128,
+                         cl, c->n_cond, c->cond_dim, c->cond_total, c->tproj.as<float>(), st);
+    const float *cproj = nullptr;
+    int64_t cstride = 0;
+    if (d.context_dim > 0) {
+        const int64_t rows = context_shared ? 1 : batch;
+        if ((rc = c->cproj.ensure(sizeof(float) * (size_t)rows * c->cond_total))) return rc;
+        launch_ctx_prologue(context, rows, d.context_dim, cl, c->n_cond, c->cond_dim, c->cond_total,
+                            c->cproj.as<float>(), st);
+        cproj = c->cproj.as<float>();
+        cstride = context_shared ? 0 : c->cond_total;
+    }
+    MlpSampleArgs m{};
+    m.wpack = c->wpack.as<float>();
+    m.plan = c->plan.as<StepPlan>();
+    m.tproj = c->tproj.as<float>();
+    m.cproj = cproj;
+    m.cproj_stride = cstride;
+    m.noise = x;
+    m.x_out = eps_cond;
+    m.chain = eps_uncond;
+    m.batch = batch;
+    m.n_steps = 1;
+    m.mode = cfg ? MODE_EPS : MODE_EPS1;
+    m.dbg = c->dbg;
+    HIP_TRY(launch_mlp_sampler(d.horizon * d.state_dim, cfg ? 2 : 1, m, st));
+    return MPCD_OK;
+}
+
+// Not part of the public header: route per-layer activations of the next mpcd_eps (block 0) to dbg.
+int mpcd_debug_set(mpcd_ctx *c, float *dbg)
+{
+    if (!c) return fail(MPCD_EINVAL, "null ctx");
+    c->dbg = dbg;
+    return MPCD_OK;
+}
+
+int mpcd_last_sample_ms(mpcd_ctx *c, float *ms)
+{
+    if (!c || !ms) return fail(MPCD_EINVAL, "null argument");
+    if (!c->timed) return fail(MPCD_ESTATE, "no sample call recorded");
+    HIP_TRY(hipEventSynchronize(c->ev1));
+    HIP_TRY(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return MPCD_OK;
+}
+
+int mpcd_clip_flag(mpcd_ctx *c, const float *x, int64_t n, int32_t *flag, void *stream_ptr)
+{
+    if (!c || !x || !flag || n < 1) return fail(MPCD_EINVAL, "bad clip_flag arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_clip_flag(x, n, flag, static_cast<hipStream_t>(stream_ptr)));
+    return MPCD_OK;
+}
+
+int mpcd_rollout_cost(mpcd_ctx *c, const mpcd_system_desc *sys, const double *x0, const float *u_norm,
+                      const float *umin, const float *umax, int64_t batch, int32_t horizon, const int32_t *clip_flag,
+                      double *cost, void *stream_ptr)
+{
+    if (!c || !sys || !x0 || !u_norm || !umin || !umax || !cost) return fail(MPCD_EINVAL, "null argument");
+    if (batch < 1 || horizon < 2) return fail(MPCD_EINVAL, "batch/horizon");
+    if (sys->n_x < 1 || sys->n_x > 12 || sys->n_u < 1 || sys->n_u > 4) return fail(MPCD_EINVAL, "n_x/n_u");
+    if (sys->system < 0 || sys->system > MPCD_SYS_QUADROTOR12) return fail(MPCD_EINVAL, "system %d", sys->system);
+    if (sys->cost_kind == MPCD_COST_CALMPC && (sys->n_u != 1 || horizon < 3))
+        return fail(MPCD_EINVAL, "calMPCCost needs n_u == 1 and H >= 3");
+    if ((size_t)horizon * sys->n_u * 64 * sizeof(float) > 64 * 1024) return fail(MPCD_EUNSUP, "H*n_u too large");
+    hipStream_t st = static_cast<hipStream_t>(stream_ptr);
+    HIP_TRY(hipSetDevice(c->device));
+    const int *flag = clip_flag;
+    if (!flag) {
+        HIP_TRY(launch_clip_flag(u_norm, batch * horizon * sys->n_u, c->flag.as<int>(), st));
+        flag = c->flag.as<int>();
+    }
+    HIP_TRY(launch_rollout_cost(*sys, x0, u_norm, umin, umax, flag, batch, horizon, cost, st));
+    return MPCD_OK;
+}
+
+int mpcd_unnormalize(mpcd_ctx *c, const float *x, int64_t n_rows, int32_t dim, const float *mn, const float *mx,
+                     const int32_t *clip_flag, float *out, void *stream_ptr)
+{
+    if (!c || !x || !mn || !mx || !out) return fail(MPCD_EINVAL, "null argument");
+    if (dim < 1 || dim > 16 || n_rows < 1) return fail(MPCD_EINVAL, "dim must be 1..16");
+    hipStream_t st = static_cast<hipStream_t>(stream_ptr);
+    HIP_TRY(hipSetDevice(c->device));
+    const int *flag = clip_flag;
+    if (!flag) {
+        HIP_TRY(launch_clip_flag(x, n_rows * dim, c->flag.as<int>(), st));
+        flag = c->flag.as<int>();
+    }
+    HIP_TRY(launch_unnormalize(x, n_rows * dim, dim, flag, mn, mx, out, st));
+    return MPCD_OK;
+}
+
+int mpcd_argmin(mpcd_ctx *c, const double *cost, int64_t n, int64_t offset, mpcd_best *best, void *stream_ptr)
+{
+    if (!c || !cost || !best || n < 1) return fail(MPCD_EINVAL, "bad argmin arguments");
+    hipStream_t st = static_cast<hipStream_t>(stream_ptr);
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_argmin(cost, n, offset, best, st));
+    return MPCD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,281 @@
+// Candidate rollout + MPC cost + selection, fp64, one thread per candidate.
+//
+// Per candidate: u = LimitsNormalizer.unnormalize(u_norm) in fp32 (normalization.py:156-167, with
+// the GLOBAL clip rule computed by clip_flag_kernel), cast exactly to fp64, then the system's
+// Euler / ZOH rollout and the MPC objective in fp64 with the reference's left-to-right operation
+// order (built with -ffp-contract=off, so no contraction changes a rounding).
+// Coalescing: a workgroup stages its candidates' [H][n_u] rows through LDS with contiguous
+// loads; each thread then walks its own row from LDS.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include <algorithm>
+
+#include "../../include/mpcd.h"
+#include "internal.h"
+
+namespace {
+
+constexpr int RT_THREADS = 64;  // candidates per workgroup
+
+struct SysK {
+    int32_t system, cost_kind, nx, nu;
+    double params[24];
+    double Q[12], R[4], P[12], xr[12];
+    double x0[12];
+    float umin[4], umax[4];
+};
+
+struct MinMax {
+    float mn[16], mx[16];
+};
+
+__device__ __forceinline__ double quadform(const double *w, const double *x, const double *ref, int n)
+{
+    double s = 0.0;
+    for (int j = 0; j < n; ++j) {
+        const double e = x[j] - ref[j];
+        s = s + w[j] * (e * e);
+    }
+    return s;
+}
+
+// x_{k+1} = f(x_k, u_k). Parameter layouts are filled by mpc_via_diffusion_model_amd/systems.py.
+__device__ __forceinline__ void dyn_step(const SysK &S, const double *x, const double *u, double *xn)
+{
+    const double *p = S.params;
+    switch (S.system) {
+    case MPCD_SYS_CARTPOLE_LIN5: {
+        // EulerForwardCartpole_virtual, xdot_new (Cart_Diffusion_inference.py:183-197)
+        // p: dt, -k*v2, (lm^2)*G*v2/il, lm*c*v2/il, v2, -l*m*k*v1/(M+m), lm*G*v1, c*v1, lm*v1/(M+m), 2/pi, pi
+        double xd[5];
+        xd[0] = x[1];
+        xd[1] = p[1] * x[1] + p[2] * x[2] - p[3] * x[3] + p[4] * u[0];
+        xd[2] = x[3];
+        xd[3] = p[5] * x[1] + p[6] * x[2] - p[7] * x[3] + p[8] * u[0];
+        xd[4] = -p[9] * (x[2] - p[10]) * x[3];
+        for (int i = 0; i < 5; ++i) xn[i] = x[i] + xd[i] * p[0];
+        break;
+    }
+    case MPCD_SYS_CARTPOLE_NL5: {
+        // nmpc_multi_process_collect_data.py:121-137. p: dt, MPLP, MPG, M_TOTAL, M_POLE, MTG, MTLP, 2/pi, pi
+        const double s = sin(x[2]), c = cos(x[2]);
+        const double dd = p[3] - p[4] * c;
+        double xd[5];
+        xd[0] = x[1];
+        xd[1] = (p[1] * -s * (x[3] * x[3]) + p[2] * s * c + u[0]) / (dd * dd);
+        xd[2] = x[3];
+        xd[3] = (-p[1] * s * c * (x[3] * x[3]) - p[5] * s - c * u[0]) / (p[6] - p[1] * (c * c));
+        xd[4] = -p[7] * (x[2] - p[8]) * x[3];
+        for (int i = 0; i < 5; ++i) xn[i] = x[i] + xd[i] * p[0];
+        break;
+    }
+    case MPCD_SYS_CARTPOLE_ZOH4:
+        // Diffusion_MPC_Inference.py:74-82. p: A_d row-major [16], B_d [4]
+        for (int i = 0; i < 4; ++i)
+            xn[i] = p[4 * i] * x[0] + p[4 * i + 1] * x[1] + p[4 * i + 2] * x[2] + p[4 * i + 3] * x[3] + p[16 + i] * u[0];
+        break;
+    case MPCD_SYS_DOUBLE_INT2D:
+        // p: dt, 0.5*dt*dt
+        xn[0] = x[0] + p[0] * x[2] + p[1] * u[0];
+        xn[1] = x[1] + p[0] * x[3] + p[1] * u[1];
+        xn[2] = x[2] + p[0] * u[0];
+        xn[3] = x[3] + p[0] * u[1];
+        break;
+    case MPCD_SYS_PENDULUM:
+        // p: dt, g/l, damping, 1/(m l^2)
+        xn[0] = x[0] + p[0] * x[1];
+        xn[1] = x[1] + p[0] * (-p[1] * sin(x[0]) - p[2] * x[1] + p[3] * u[0]);
+        break;
+    case MPCD_SYS_QUADROTOR12: {
+        // p: dt, m, g, Ix, Iy, Iz
+        const double sph = sin(x[3]), cph = cos(x[3]), sth = sin(x[4]), cth = cos(x[4]);
+        const double sps = sin(x[5]), cps = cos(x[5]);
+        const double f_m = (p[1] * p[2] + u[0]) / p[1];
+        double xd[12];
+        xd[0] = x[6];
+        xd[1] = x[7];
+        xd[2] = x[8];
+        xd[3] = x[9] + (x[10] * sph + x[11] * cph) * (sth / cth);
+        xd[4] = x[10] * cph - x[11] * sph;
+        xd[5] = (x[10] * sph + x[11] * cph) / cth;
+        xd[6] = f_m * (cph * sth * cps + sph * sps);
+        xd[7] = f_m * (cph * sth * sps - sph * cps);
+        xd[8] = f_m * (cph * cth) - p[2];
+        xd[9] = ((p[4] - p[5]) * x[10] * x[11] + u[1]) / p[3];
+        xd[10] = ((p[5] - p[3]) * x[9] * x[11] + u[2]) / p[4];
+        xd[11] = ((p[3] - p[4]) * x[9] * x[10] + u[3]) / p[5];
+        for (int i = 0; i < 12; ++i) xn[i] = x[i] + p[0] * xd[i];
+        break;
+    }
+    default:
+        for (int i = 0; i < S.nx; ++i) xn[i] = NAN;
+    }
+}
+
+// any |u_norm| outside [-1-eps, 1+eps]  ->  *flag = 1   (x.max() > 1+eps or x.min() < -1-eps)
+__global__ void clip_flag_kernel(const float *x, int64_t n, int *flag)
+{
+    const float hi = (float)(1.0 + 1e-4), lo = (float)(-1.0 - 1e-4);
+    int any = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float v = x[i];
+        any |= (v > hi) | (v < lo);
+    }
+    if (__any(any) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+__device__ __forceinline__ float unnorm1(float v, bool clip, float mn, float mx)
+{
+    if (clip) v = fminf(fmaxf(v, -1.0f), 1.0f);
+    const float h = (v + 1.0f) / 2.0f;
+    return h * (mx - mn) + mn;
+}
+
+__global__ void unnormalize_kernel(const float *x, int64_t n, int dim, const int *flag, const MinMax lim, float *out)
+{
+    const bool clip = *flag != 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % dim);
+        out[i] = unnorm1(x[i], clip, lim.mn[c], lim.mx[c]);
+    }
+}
+
+__global__ __launch_bounds__(RT_THREADS) void rollout_cost_kernel(const SysK S, const float *u_norm, const int *flag,
+                                                                  int64_t batch, int H, double *cost)
+{
+    extern __shared__ float su[];  // [RT_THREADS][H*nu + 1]
+    const int row = H * S.nu, stride = row + 1;
+    const int64_t c0 = (int64_t)blockIdx.x * RT_THREADS;
+    const int64_t nvalid = min((int64_t)RT_THREADS, batch - c0);
+    const float *src = u_norm + (size_t)c0 * row;
+    for (int i = threadIdx.x; i < nvalid * row; i += RT_THREADS) {
+        const int c = i / row, k = i - c * row;
+        su[c * stride + k] = src[i];
+    }
+    __syncthreads();
+    const int64_t b = c0 + threadIdx.x;
+    if (b >= batch) return;
+    const bool clip = *flag != 0;
+    float mn[4], mx[4];
+    for (int i = 0; i < S.nu; ++i) { mn[i] = S.umin[i]; mx[i] = S.umax[i]; }
+    const float *ur = su + threadIdx.x * stride;
+    const int nx = S.nx, nu = S.nu;
+    double x[12], xn[12], u[4];
+    for (int i = 0; i < nx; ++i) x[i] = S.x0[i];
+    double J;
+    if (S.cost_kind == MPCD_COST_CALMPC) {
+        // calMPCCost (Cart_Diffusion_inference.py:247-283); num_u = 1 (batch axis of u_hor)
+        J = 0.0;
+        for (int i = 0; i < nx; ++i) J = J + S.Q[i] * (x[i] * x[i]);
+        u[0] = (double)unnorm1(ur[0], clip, mn[0], mx[0]);
+        J = J + S.R[0] * (u[0] * u[0]);
+        for (int i = 0; i < nx; ++i) xn[i] = x[i];
+        double ucur = u[0];
+        for (int i = 1; i < H - 1; ++i) {
+            dyn_step(S, x, &ucur, xn);
+            const double un = (double)unnorm1(ur[i * nu], clip, mn[0], mx[0]);
+            for (int j = 1; j < nx; ++j) J = J + S.Q[j] * (xn[j] * xn[j]);
+            J = J + S.R[0] * (un * un);
+            ucur = un;
+            for (int j = 0; j < nx; ++j) x[j] = xn[j];
+        }
+        for (int i = 0; i < nx; ++i) J = J + S.P[i] * (xn[i] * xn[i]);
+    } else {
+        const double zero[4] = {0.0, 0.0, 0.0, 0.0};
+        J = quadform(S.Q, x, S.xr, nx);
+        for (int k = 0; k < H; ++k) {
+            for (int i = 0; i < nu; ++i) u[i] = (double)unnorm1(ur[k * nu + i], clip, mn[i], mx[i]);
+            dyn_step(S, x, u, xn);
+            const double sx = k < H - 1 ? quadform(S.Q, xn, S.xr, nx) : quadform(S.P, xn, S.xr, nx);
+            const double sv = quadform(S.R, u, zero, nu);
+            J = J + (sx + sv);
+            for (int j = 0; j < nx; ++j) x[j] = xn[j];
+        }
+    }
+    cost[b] = J;
+}
+
+// Single-workgroup argmin: NaN -> +inf; ties -> lowest index.
+__global__ __launch_bounds__(1024) void argmin_kernel(const double *cost, int64_t n, int64_t offset, mpcd_best *best)
+{
+    __shared__ double sv[1024];
+    __shared__ int64_t si[1024];
+    double bv = INFINITY;
+    int64_t bi = -1;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        double v = cost[i];
+        if (isnan(v)) v = INFINITY;
+        if (bi < 0 || v < bv) { bv = v; bi = i; }
+    }
+    sv[threadIdx.x] = bv;
+    si[threadIdx.x] = bi;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+            const double ov = sv[threadIdx.x + w];
+            const int64_t oi = si[threadIdx.x + w];
+            const double mv = sv[threadIdx.x];
+            const int64_t mi = si[threadIdx.x];
+            const bool take = oi >= 0 && (mi < 0 || ov < mv || (ov == mv && oi < mi));
+            if (take) { sv[threadIdx.x] = ov; si[threadIdx.x] = oi; }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        best->cost = sv[0];
+        best->index = si[0] < 0 ? -1 : offset + si[0];
+    }
+}
+
+}  // namespace
+
+hipError_t launch_clip_flag(const float *x, int64_t n, int *flag_dev, hipStream_t stream)
+{
+    hipError_t e = hipMemsetAsync(flag_dev, 0, sizeof(int), stream);
+    if (e != hipSuccess) return e;
+    const int64_t blocks = std::min<int64_t>(1024, (n + 255) / 256);
+    hipLaunchKernelGGL(clip_flag_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, stream, x, n, flag_dev);
+    return hipGetLastError();
+}
+
+hipError_t launch_unnormalize(const float *x, int64_t n, int dim, const int *flag_dev, const float *mn_host,
+                              const float *mx_host, float *out, hipStream_t stream)
+{
+    MinMax lim;
+    for (int i = 0; i < 16; ++i) {
+        lim.mn[i] = i < dim ? mn_host[i] : 0.f;
+        lim.mx[i] = i < dim ? mx_host[i] : 0.f;
+    }
+    const int64_t blocks = std::min<int64_t>(4096, (n + 255) / 256);
+    hipLaunchKernelGGL(unnormalize_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, stream, x, n,
+                       dim, flag_dev, lim, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_rollout_cost(const mpcd_system_desc &d, const double *x0_host, const float *u_norm,
+                               const float *umin_host, const float *umax_host, const int *flag_dev, int64_t batch, int H,
+                               double *cost, hipStream_t stream)
+{
+    SysK S = {};
+    S.system = d.system;
+    S.cost_kind = d.cost_kind;
+    S.nx = d.n_x;
+    S.nu = d.n_u;
+    for (int i = 0; i < 24; ++i) S.params[i] = d.params[i];
+    for (int i = 0; i < 12; ++i) { S.Q[i] = d.Q[i]; S.P[i] = d.P[i]; S.xr[i] = d.x_ref[i]; }
+    for (int i = 0; i < 4; ++i) S.R[i] = d.R[i];
+    for (int i = 0; i < d.n_x; ++i) S.x0[i] = x0_host[i];
+    for (int i = 0; i < d.n_u; ++i) { S.umin[i] = umin_host[i]; S.umax[i] = umax_host[i]; }
+    const size_t lds = sizeof(float) * RT_THREADS * (H * d.n_u + 1);
+    const int64_t blocks = (batch + RT_THREADS - 1) / RT_THREADS;
+    hipLaunchKernelGGL(rollout_cost_kernel, dim3((unsigned)blocks), dim3(RT_THREADS), lds, stream, S, u_norm, flag_dev,
+                       batch, H, cost);
+    return hipGetLastError();
+}
+
+hipError_t launch_argmin(const double *cost, int64_t n, int64_t offset, mpcd_best *best, hipStream_t stream)
+{
+    hipLaunchKernelGGL(argmin_kernel, dim3(1), dim3(1024), 0, stream, cost, n, offset, best);
+    return hipGetLastError();
+}

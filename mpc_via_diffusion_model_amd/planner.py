@@ -1,0 +1,318 @@
+"""Diffusion-MPC planner: the reference's operator API over the MI355X HIP kernels.
+
+Drop-in for the control-loop body of scripts/inference/Diffusion_MPC_Inference.py:191-289 and
+Cart_Diffusion_inference.py:405-512:
+
+  reference                                             here
+  GaussianDiffusionModel(model=..., ...) + load_state_dict  DiffusionMPC.from_state_dict(sd, spec)
+  dataset.normalize_condition(x0)                        DiffusionMPC.normalize_condition(x0)
+  model.run_CFG(context, hard_conds, w, n_samples, horizon, return_chain, sample_fn, n_wo)
+                                                         DiffusionMPC.run_CFG(...)   (same signature)
+  dataset.unnormalize_states(chain)                      DiffusionMPC.unnormalize_states(x)
+  calMPCCost / MPC objective per sample, argmin          DiffusionMPC.mpc_step(x0, system, n_samples)
+  (no reference name)                                    DiffusionMPC.sample_trajectories(...)
+
+All compute runs in libmpcd.so (HIP, gfx950); torch supplies device memory, the current stream and
+torch.distributed. There is no CPU fallback: a missing library or a failing call raises.
+"""
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _native as N
+from . import distributed as D
+from . import schedule as S
+from .systems import System
+
+_SAMPLERS = {"ddpm_cfg": N.MPCD_DDPM_CFG, "ddpm_cart_pole_sample_fn": N.MPCD_DDPM_CFG,
+             "ddim_cfg": N.MPCD_DDIM_CFG, "ddim": N.MPCD_DDIM, "ddim_sample": N.MPCD_DDIM}
+
+
+@dataclass
+class NetSpec:
+    """Architecture of the noise-net (temporal_unet.py constructor arguments)."""
+    kind: str                 # "mlp" (build-defined CFG MLP) or "unet" (ConditionedTemporalUnet / TemporalUnet)
+    state_dim: int            # d
+    horizon: int              # H
+    context_dim: int          # C (0: TemporalUnet with conditioning None)
+    base_dim: int = 32        # unet_input_dim
+    dim_mults: tuple = (1, 2, 4)
+    time_emb_dim: int = 32
+    cfg: bool = True          # 4-arg net with the CFG context mask
+    dtype: str = "f32"
+
+    def desc(self):
+        d = N.NetDesc()
+        d.kind = N.MPCD_NET_MLP if self.kind == "mlp" else N.MPCD_NET_UNET
+        d.state_dim, d.horizon, d.context_dim = self.state_dim, self.horizon, self.context_dim
+        d.base_dim, d.n_mults = self.base_dim, len(self.dim_mults)
+        for i, m in enumerate(self.dim_mults):
+            d.mults[i] = m
+        d.time_emb_dim = self.time_emb_dim
+        d.cfg_masked = 1 if self.cfg else 0
+        d.dtype = N.MPCD_F16 if self.dtype == "f16" else N.MPCD_F32
+        return d
+
+
+@dataclass
+class MPCResult:
+    u0: np.ndarray          # [d] applied action, unnormalised
+    u_best: np.ndarray      # [H, d] winning trajectory, unnormalised
+    best_cost: float
+    best_index: int         # global candidate index
+    costs: torch.Tensor     # [B_total] fp64 on device (all ranks' candidates)
+    u_norm: torch.Tensor    # [B_local, H, d] this rank's normalised samples
+
+
+class DiffusionMPC:
+    def __init__(self, spec, params, tables=None, variance_schedule="exponential", n_diffusion_steps=100,
+                 device=None, context_limits=None, action_limits=None):
+        """params: dict name -> tensor (module state_dict keys, no "model." prefix) in any order.
+        tables: dict of the 12 diffusion buffers (e.g. from a checkpoint) or None to compute them."""
+        self.spec = spec
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self.n_steps = n_diffusion_steps if tables is None else int(tables["betas"].numel())
+        self.tables = tables if tables is not None else S.tables(variance_schedule, n_diffusion_steps)
+        if not S.is_finite(self.tables):
+            raise ValueError(f"{variance_schedule} schedule with N={self.n_steps} is not finite "
+                             "(the reference would produce NaN; use 'cosine' or another N)")
+        c_lo, c_hi = context_limits if context_limits is not None else (-np.ones(spec.context_dim),
+                                                                        np.ones(spec.context_dim))
+        a_lo, a_hi = action_limits if action_limits is not None else (-np.ones(spec.state_dim),
+                                                                      np.ones(spec.state_dim))
+        self.ctx_min = np.asarray(c_lo, dtype=np.float32)
+        self.ctx_max = np.asarray(c_hi, dtype=np.float32)
+        self.act_min = np.ascontiguousarray(a_lo, dtype=np.float32)
+        self.act_max = np.ascontiguousarray(a_hi, dtype=np.float32)
+        self._lib = N.lib()
+        self._ctx = ctypes.c_void_p()
+        N.check(self._lib.mpcd_create(self.device.index, ctypes.byref(self._ctx)), "mpcd_create")
+        self._desc = spec.desc()
+        self.param_spec = N.param_spec(self._desc)
+        blob = torch.cat([params[n].detach().to("cpu", torch.float32).reshape(-1) for n, _ in self.param_spec])
+        for n, shp in self.param_spec:
+            if tuple(params[n].shape) != shp:
+                raise ValueError(f"{n}: shape {tuple(params[n].shape)} != {shp}")
+        blob = blob.contiguous()
+        N.check(self._lib.mpcd_load_net(self._ctx, ctypes.byref(self._desc), ctypes.c_void_p(blob.data_ptr()),
+                                        blob.numel()), "mpcd_load_net")
+        tab = S.pack(self.tables)
+        std = S.posterior_std(self.tables).contiguous()
+        N.check(self._lib.mpcd_set_schedule(self._ctx, ctypes.c_void_p(tab.data_ptr()), self.n_steps,
+                                            ctypes.c_void_p(std.data_ptr())), "mpcd_set_schedule")
+        # DDPM with clip_denoised ends with x = coef1[0]*clamp(x0) + coef2[0]*x: if coef2[0] == 0 and
+        # |coef1[0]| <= 1 + 1e-4 the unnormalise clip flag is provably 0 for every candidate.
+        c1, c2 = float(self.tables["posterior_mean_coef1"][0]), float(self.tables["posterior_mean_coef2"][0])
+        self.ddpm_final_in_range = c2 == 0.0 and abs(c1) <= np.float32(1 + 1e-4)
+        self._flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._best = torch.zeros(2, dtype=torch.float64, device=self.device)  # mpcd_best {double, int64}
+
+    # ------------------------------------------------------------------ construction helpers
+    @classmethod
+    def from_state_dict(cls, state_dict, spec, **kw):
+        """Reference checkpoint layout: "model.<param>" + the 12 schedule buffers (weights-only load)."""
+        has_prefix = any(k.startswith("model.") for k in state_dict)
+        params = {k[6:] if has_prefix and k.startswith("model.") else k: v for k, v in state_dict.items()}
+        tables = None
+        if all(k in state_dict for k in S.TABLE_ORDER):
+            tables = {k: state_dict[k].detach().cpu().to(torch.float32) for k in S.TABLE_ORDER}
+        return cls(spec, params, tables=tables, **kw)
+
+    def close(self):
+        if getattr(self, "_ctx", None) and self._ctx.value:
+            self._lib.mpcd_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ normalisation (A12)
+    def normalize_condition(self, x0):
+        """LimitsNormalizer.normalize of the fp64 state (normalization.py:149-154), cast to fp32 as the
+        net's c_emb.float() does (temporal_unet.py:314). Host-side: C values per control step."""
+        x = np.asarray(x0, dtype=np.float64)
+        mn = self.ctx_min.astype(np.float64)
+        den = (self.ctx_max - self.ctx_min).astype(np.float64)  # fp32 subtraction, then promoted
+        return (2 * ((x - mn) / den) - 1).astype(np.float32)
+
+    def unnormalize_states(self, x, clip_flag=None):
+        """LimitsNormalizer.unnormalize on device (normalization.py:156-167), global clip rule."""
+        x = x.contiguous()
+        out = torch.empty_like(x)
+        d = x.shape[-1]
+        flag_ptr = ctypes.c_void_p(clip_flag.data_ptr()) if clip_flag is not None else None
+        N.check(self._lib.mpcd_unnormalize(self._ctx, ctypes.c_void_p(x.data_ptr()), x.numel() // d, d,
+                                           self.act_min.ctypes.data, self.act_max.ctypes.data, flag_ptr,
+                                           ctypes.c_void_p(out.data_ptr()), self._stream()), "mpcd_unnormalize")
+        return out
+
+    # ------------------------------------------------------------------ sampling (A2-A11)
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _sampler_id(self, sample_fn):
+        name = sample_fn if isinstance(sample_fn, str) else getattr(sample_fn, "__name__", str(sample_fn))
+        if name not in _SAMPLERS:
+            raise ValueError(f"unsupported sample_fn {name!r}; use one of {sorted(_SAMPLERS)}")
+        return _SAMPLERS[name]
+
+    def _args(self, sampler, batch, context, w, n_wo_noise, ddim_steps, clamp_x0, seed, global_offset, noise,
+              x_out, chain):
+        a = N.SampleArgs()
+        if self.spec.context_dim > 0:
+            if context is None:
+                raise ValueError("this net needs a context")
+            a.context = context.data_ptr()
+            a.context_shared = 1 if context.shape[0] == 1 else 0
+            if not a.context_shared and context.shape[0] != batch:
+                raise ValueError(f"context rows {context.shape[0]} must be 1 or n_samples={batch}")
+        a.sampler = sampler
+        a.batch = batch
+        a.w = float(w)
+        a.n_wo_noise = int(n_wo_noise)
+        a.ddim_steps = int(ddim_steps or 0)
+        a.clamp_x0 = 1 if clamp_x0 else 0
+        if sampler != N.MPCD_DDPM_CFG:
+            times = S.ddim_times(self.n_steps, ddim_steps or None)
+            self._times = (ctypes.c_int32 * len(times))(*times)
+            a.ddim_times = ctypes.cast(self._times, ctypes.POINTER(ctypes.c_int32))
+            a.n_ddim_times = len(times)
+        a.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        a.global_offset = int(global_offset)
+        a.noise = noise.data_ptr() if noise is not None else None
+        a.x_out = x_out.data_ptr()
+        a.chain_out = chain.data_ptr() if chain is not None else None
+        return a
+
+    def n_denoise_steps(self, sample_fn="ddpm_cfg", n_wo_noise=0, ddim_steps=None):
+        a = N.SampleArgs()
+        a.sampler = self._sampler_id(sample_fn)
+        a.n_wo_noise = n_wo_noise
+        a.ddim_steps = int(ddim_steps or 0)
+        if a.sampler != N.MPCD_DDPM_CFG:
+            times = S.ddim_times(self.n_steps, ddim_steps or None)
+            self._times = (ctypes.c_int32 * len(times))(*times)
+            a.ddim_times = ctypes.cast(self._times, ctypes.POINTER(ctypes.c_int32))
+            a.n_ddim_times = len(times)
+        n = ctypes.c_int32()
+        N.check(self._lib.mpcd_sample_steps(self._ctx, ctypes.byref(a), ctypes.byref(n)), "mpcd_sample_steps")
+        return n.value
+
+    def sample_trajectories(self, context=None, n_samples=1, horizon=None, w=0.01, sample_fn="ddpm_cfg",
+                            n_wo_noise=0, ddim_steps=None, clamp_x0=False, seed=0, global_offset=0, noise=None,
+                            return_chain=False, out=None):
+        """Normalised candidate trajectories [B, H, d] (or the chain [S+1, B, H, d]).
+        context: [1, C] (shared) or [B, C] normalised fp32; noise: optional injected [S+1, B, H, d]."""
+        H = horizon or self.spec.horizon
+        if H != self.spec.horizon:
+            raise ValueError(f"net was built for horizon {self.spec.horizon}")
+        sampler = self._sampler_id(sample_fn)
+        B = int(n_samples)
+        d = self.spec.state_dim
+        if context is not None:
+            context = torch.as_tensor(context, dtype=torch.float32)
+            if context.dim() == 1:
+                context = context[None]
+            context = context.to(self.device).contiguous()
+        steps = self.n_denoise_steps(sample_fn, n_wo_noise, ddim_steps)
+        if noise is not None:
+            noise = noise.to(self.device, torch.float32).contiguous()
+            if tuple(noise.shape) != (steps + 1, B, H, d):
+                raise ValueError(f"noise must be [{steps + 1}, {B}, {H}, {d}], got {tuple(noise.shape)}")
+        x = out if out is not None else torch.empty((B, H, d), dtype=torch.float32, device=self.device)
+        chain = torch.empty((steps + 1, B, H, d), dtype=torch.float32, device=self.device) if return_chain else None
+        a = self._args(sampler, B, context, w, n_wo_noise, ddim_steps, clamp_x0, seed, global_offset, noise, x, chain)
+        N.check(self._lib.mpcd_sample(self._ctx, ctypes.byref(a), self._stream()), "mpcd_sample")
+        return chain if return_chain else x
+
+    def run_CFG(self, context=None, hard_conds=None, context_weight=0.1, n_samples=1, horizon=8,
+                return_chain=False, sample_fn="ddpm_cart_pole_sample_fn", n_diffusion_steps_without_noise=0,
+                noise=None, seed=0, **_unused):
+        """GaussianDiffusionModel.run_CFG (diffusion_model_base.py:394-418): chain [S+1, B, H, d] or
+        the final [B, H, d], normalised. hard_conds is ignored as in the reference (commented out there)."""
+        return self.sample_trajectories(context, n_samples, horizon, context_weight, sample_fn,
+                                        n_diffusion_steps_without_noise, noise=noise, seed=seed,
+                                        return_chain=return_chain)
+
+    def eps(self, x, t, context=None):
+        """Noise-net forward(s) at time t: (eps_cond, eps_uncond) for a CFG net, (eps, None) otherwise."""
+        x = x.to(self.device, torch.float32).contiguous()
+        B = x.shape[0]
+        if context is not None:
+            context = torch.as_tensor(context, dtype=torch.float32).to(self.device).contiguous()
+            if context.dim() == 1:
+                context = context[None]
+        ec = torch.empty_like(x)
+        eu = torch.empty_like(x) if self.spec.cfg else None
+        N.check(self._lib.mpcd_eps(self._ctx, ctypes.c_void_p(x.data_ptr()), int(t),
+                                   ctypes.c_void_p(context.data_ptr()) if context is not None else None,
+                                   1 if context is not None and context.shape[0] == 1 else 0, B,
+                                   ctypes.c_void_p(ec.data_ptr()), ctypes.c_void_p(eu.data_ptr()) if eu is not None else None,
+                                   self._stream()), "mpcd_eps")
+        return ec, eu
+
+    def last_sample_ms(self):
+        ms = ctypes.c_float()
+        N.check(self._lib.mpcd_last_sample_ms(self._ctx, ctypes.byref(ms)), "mpcd_last_sample_ms")
+        return ms.value
+
+    # ------------------------------------------------------------------ rollout / cost / selection (A13-A15)
+    def rollout_cost(self, system: System, x0, u_norm, clip_flag=None):
+        """fp64 cost per candidate [B] on device."""
+        B, H, d = u_norm.shape
+        if d != system.n_u:
+            raise ValueError(f"system {system.name} has {system.n_u} inputs, samples have {d}")
+        x0 = np.ascontiguousarray(x0, dtype=np.float64)
+        cost = torch.empty(B, dtype=torch.float64, device=self.device)
+        desc = system.desc()
+        flag_ptr = ctypes.c_void_p(clip_flag.data_ptr()) if clip_flag is not None else None
+        N.check(self._lib.mpcd_rollout_cost(self._ctx, ctypes.byref(desc), x0.ctypes.data,
+                                            ctypes.c_void_p(u_norm.contiguous().data_ptr()), self.act_min.ctypes.data,
+                                            self.act_max.ctypes.data, B, H, flag_ptr, ctypes.c_void_p(cost.data_ptr()),
+                                            self._stream()), "mpcd_rollout_cost")
+        return cost
+
+    def clip_flag(self, x):
+        flag = torch.empty(1, dtype=torch.int32, device=self.device)
+        N.check(self._lib.mpcd_clip_flag(self._ctx, ctypes.c_void_p(x.data_ptr()), x.numel(),
+                                         ctypes.c_void_p(flag.data_ptr()), self._stream()), "mpcd_clip_flag")
+        return flag
+
+    def argmin(self, cost, index_offset=0):
+        """Device argmin (NaN = +inf, lowest index on ties) -> (index, cost); syncs the stream."""
+        N.check(self._lib.mpcd_argmin(self._ctx, ctypes.c_void_p(cost.data_ptr()), cost.numel(), index_offset,
+                                      ctypes.c_void_p(self._best.data_ptr()), self._stream()), "mpcd_argmin")
+        host = self._best.cpu()
+        return int(host.view(torch.int64)[1]), float(host[0])
+
+    def mpc_step(self, x0, system: System, n_samples, w=0.01, sample_fn="ddpm_cfg", n_wo_noise=0, ddim_steps=None,
+                 clamp_x0=False, seed=0, noise=None, group=None):
+        """One control step: sample n_samples candidates on this rank (weak scaling: every rank adds
+        n_samples), roll out + cost them, all-gather costs, pick the global argmin, broadcast it."""
+        rank, size = D.world(group)
+        offset, total = D.shard(n_samples, group)
+        ctx = torch.from_numpy(self.normalize_condition(x0)[None])
+        u_norm = self.sample_trajectories(ctx, n_samples, self.spec.horizon, w, sample_fn, n_wo_noise, ddim_steps,
+                                          clamp_x0, seed, offset, noise)
+        flag = None
+        sampler = self._sampler_id(sample_fn)
+        if size > 1 and not (sampler == N.MPCD_DDPM_CFG and self.ddpm_final_in_range):
+            flag = D.any_flag(self.clip_flag(u_norm), group)
+        cost_local = self.rollout_cost(system, x0, u_norm, flag)
+        costs = D.gather_costs(cost_local, group)
+        idx, best = self.argmin(costs)
+        owner, local = divmod(idx, n_samples)
+        row = D.broadcast_row(u_norm[local if owner == rank else 0], owner, group)
+        if flag is None and size == 1:
+            u_best = self.unnormalize_states(row[None], self.clip_flag(u_norm))[0]
+        else:
+            u_best = self.unnormalize_states(row[None], flag if flag is not None else
+                                             torch.zeros(1, dtype=torch.int32, device=self.device))[0]
+        u_host = u_best.cpu().numpy()
+        return MPCResult(u0=u_host[0].copy(), u_best=u_host, best_cost=best, best_index=idx, costs=costs,
+                         u_norm=u_norm)

@@ -1,0 +1,144 @@
+"""GPU parity: persistent MLP sampler (CFG-DDPM, CFG-DDIM, DDIM) against the oracle, via the C ABI."""
+import numpy as np
+import pytest
+import torch
+
+from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec
+from oracle import sampler as osam
+from oracle import schedule as osch
+
+from ._util import assert_traj_close, make_mlp, oracle_sensitivity
+
+pytestmark = pytest.mark.gpu
+
+
+def _planner(net, d, H, C, n_steps=100, kind="exponential", cfg=True):
+    spec = NetSpec("mlp", state_dim=d, horizon=H, context_dim=C, cfg=cfg)
+    return DiffusionMPC(spec, net.state_dict(), variance_schedule=kind, n_diffusion_steps=n_steps)
+
+
+def _ctx(B, C, shared, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    rows = 1 if shared else B
+    return torch.rand(rows, C, generator=g) * 2 - 1
+
+
+@pytest.mark.parametrize("B,H,d,C,N,nwo,shared", [
+    (64, 16, 2, 4, 50, 0, True),     # BASELINE cfg 1 shape
+    (256, 32, 2, 4, 100, 0, True),   # cfg 2 shape, oracle-sized batch
+    (100, 32, 2, 4, 100, 5, False),  # ragged batch (not a multiple of 16), per-candidate context, nwo > 0
+    (48, 64, 2, 3, 25, 3, False),    # H*d = 128
+])
+def test_ddpm_cfg_matches_oracle(B, H, d, C, N, nwo, shared):
+    net = make_mlp(d, H, C)
+    plan = _planner(net, d, H, C, N)
+    ctx = _ctx(B, C, shared)
+    S = N + nwo
+    noise = torch.randn(S + 1, B, H, d, generator=torch.Generator().manual_seed(11))
+    ref = osam.ddpm_cfg(net, osch.buffers("exponential", N), ctx.expand(B, C), 0.01, B, H, nwo, noise=noise,
+                        return_chain=True)
+    got = plan.run_CFG(ctx, None, 0.01, n_samples=B, horizon=H, return_chain=True,
+                       n_diffusion_steps_without_noise=nwo, noise=noise)
+    torch.cuda.synchronize()
+    assert tuple(got.shape) == (S + 1, B, H, d)
+    assert torch.equal(got[0].cpu(), noise[0])
+    assert_traj_close(got, ref, what="ddpm chain")
+
+
+def test_ddpm_cfg_cosine_250():
+    B, H, d, C, N = 32, 32, 2, 4, 250
+    net = make_mlp(d, H, C, seed=5)
+    plan = _planner(net, d, H, C, N, kind="cosine")
+    ctx = _ctx(B, C, True)
+    noise = torch.randn(N + 1, B, H, d, generator=torch.Generator().manual_seed(2))
+    ref = osam.ddpm_cfg(net, osch.buffers("cosine", N), ctx.expand(B, C), 0.01, B, H, noise=noise)
+    got = plan.sample_trajectories(ctx, B, H, w=0.01, noise=noise)
+    assert_traj_close(got, ref, what="cosine N=250")
+
+
+@pytest.mark.parametrize("steps,clamp", [(None, False), (20, True)])
+def test_ddim_cfg_matches_oracle(steps, clamp):
+    B, H, d, C, N = 64, 32, 2, 4, 100
+    net = make_mlp(d, H, C, seed=2)
+    plan = _planner(net, d, H, C, N)
+    ctx = _ctx(B, C, True)
+    S = len(osam.ddim_grid(N, steps))
+    noise = torch.randn(S + 1, B, H, d, generator=torch.Generator().manual_seed(4))
+    ref, spread = oracle_sensitivity(lambda: osam.ddim_cfg(net, osch.buffers("exponential", N), ctx.expand(B, C), 0.01,
+                                                           B, H, noise=noise, sampling_steps=steps, clamp_x0=clamp,
+                                                           return_chain=True))
+    got = plan.sample_trajectories(ctx, B, H, w=0.01, sample_fn="ddim_cfg", ddim_steps=steps, clamp_x0=clamp,
+                                   noise=noise, return_chain=True)
+    assert_traj_close(got[: ref.shape[0]], ref, abs_elem=max(1e-4, 4 * spread), what="ddim_cfg chain")
+
+
+def test_ddim_uncond_matches_oracle():
+    """3-arg net (context concatenated, no mask) + reference ddim_sample (unclamped)."""
+    B, H, d, C, N = 64, 32, 2, 4, 100
+    net = make_mlp(d, H, C, seed=6)
+    plan = _planner(net, d, H, C, N, cfg=False)
+    ctx = _ctx(B, C, False)
+    S = len(osam.ddim_grid(N))
+    noise = torch.randn(S + 1, B, H, d, generator=torch.Generator().manual_seed(8))
+    zeros = torch.zeros(B, 1)
+    net3 = lambda x, t, c: net(x, t, c, zeros)  # noqa: E731
+    net3.state_dim = d
+    ref, spread = oracle_sensitivity(lambda: osam.ddim(net3, osch.buffers("exponential", N), B, H, context=ctx,
+                                                       noise=noise))
+    got = plan.sample_trajectories(ctx, B, H, sample_fn="ddim", noise=noise)
+    assert_traj_close(got, ref, abs_elem=max(1e-4, 4 * spread), what="ddim")
+
+
+def test_eps_forward_both_branches():
+    """One net forward (A11) on both CFG branches vs the oracle, every layer path."""
+    B, H, d, C, N = 40, 32, 2, 4, 100
+    net = make_mlp(d, H, C, seed=12)
+    plan = _planner(net, d, H, C, N)
+    x = torch.randn(B, H, d, generator=torch.Generator().manual_seed(1))
+    for shared in (True, False):
+        ctx = _ctx(B, C, shared)
+        for t in (0, 37, 99):
+            ec, eu = plan.eps(x, t, ctx)
+            tt = torch.full((B,), t, dtype=torch.long)
+            with torch.no_grad():
+                rc = net(x, tt, ctx.expand(B, C), torch.zeros(B, 1))
+                ru = net(x, tt, ctx.expand(B, C), torch.ones(B, 1))
+            assert float((ec.cpu() - rc).abs().max()) < 5e-6
+            assert float((eu.cpu() - ru).abs().max()) < 5e-6
+
+
+def test_philox_shard_invariance_and_stats():
+    """Throughput mode: noise keyed by global candidate index -> identical results for any sharding."""
+    B, H, d, C, N = 512, 32, 2, 4, 100
+    net = make_mlp(d, H, C)
+    plan = _planner(net, d, H, C, N)
+    ctx = _ctx(B, C, True)
+    full = plan.sample_trajectories(ctx, B, H, seed=123, return_chain=True)
+    a = plan.sample_trajectories(ctx, B // 2, H, seed=123, global_offset=0, return_chain=True)
+    b = plan.sample_trajectories(ctx, B // 2, H, seed=123, global_offset=B // 2, return_chain=True)
+    torch.cuda.synchronize()
+    assert torch.equal(full, torch.cat([a, b], dim=1))
+    again = plan.sample_trajectories(ctx, B, H, seed=123, return_chain=True)
+    assert torch.equal(full, again)
+    xT = full[0].double()
+    assert abs(float(xT.mean())) < 0.02 and abs(float(xT.std()) - 1) < 0.02
+    other = plan.sample_trajectories(ctx, B, H, seed=124)
+    assert not torch.equal(full[-1], other)
+
+
+def test_full_size_cfg2_properties():
+    """BASELINE cfg 2 size (B=4096, H=32, N=100): finite, inside the clamp bound, deterministic."""
+    B, H, d, C, N = 4096, 32, 2, 4, 100
+    net = make_mlp(d, H, C)
+    plan = _planner(net, d, H, C, N)
+    ctx = _ctx(B, C, True)
+    x1 = plan.sample_trajectories(ctx, B, H, seed=7)
+    x2 = plan.sample_trajectories(ctx, B, H, seed=7)
+    torch.cuda.synchronize()
+    assert torch.isfinite(x1).all()
+    c1 = float(plan.tables["posterior_mean_coef1"][0])
+    assert float(x1.abs().max()) <= abs(c1) * (1 + 1e-6)
+    assert torch.equal(x1, x2)
+    # a 64-candidate slice equals the same candidates run alone (shard property at full size)
+    part = plan.sample_trajectories(ctx, 64, H, seed=7, global_offset=4032)
+    assert torch.equal(part, x1[4032:])

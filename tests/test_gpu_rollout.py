@@ -1,0 +1,122 @@
+"""GPU parity: fp64 rollout/cost kernel vs the C oracle, unnormalise clip rule, argmin, mpc_step."""
+import numpy as np
+import pytest
+import torch
+
+from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec, systems
+from oracle import sampler as osam
+from oracle import schedule as osch
+from oracle import systems as osys
+
+from ._util import make_mlp, unnormalize_np
+
+pytestmark = pytest.mark.gpu
+
+EXACT = {"cartpole_lin5", "cartpole_zoh4", "double_int2d"}  # no transcendental: bit-exact
+# sin/cos differ from glibc by <= 1 ulp (ocml vs libm); the quadrotor's tan/sec terms amplify that
+# over 32 steps of random, large torques (Ix = 0.01), so its bar is 1e-6 relative, the others 1e-9.
+RTOL = {"cartpole_nl5": 1e-9, "pendulum": 1e-9, "quadrotor12": 1e-6}
+
+
+def _planner(d=1, H=32, C=5, lo=-1.0, hi=1.0):
+    net = make_mlp(d, H, C)
+    return DiffusionMPC(NetSpec("mlp", state_dim=d, horizon=H, context_dim=C), net.state_dict(),
+                        n_diffusion_steps=25, action_limits=(np.full(d, lo), np.full(d, hi)))
+
+
+def _x0(name, rng):
+    n = systems.get(name).n_x
+    x = rng.uniform(-1, 1, n)
+    if name.startswith("cartpole") and n == 5:
+        x[2] = 0.9 * np.pi + 0.1 * x[2]
+        x[4] = (x[2] - np.pi) ** 2 / -np.pi + np.pi
+    return x
+
+
+@pytest.mark.parametrize("name", sorted(systems.REGISTRY))
+@pytest.mark.parametrize("spread", [0.9, 1.3])  # 1.3: global clip rule triggers
+def test_rollout_cost_matches_c_oracle(name, spread):
+    sysd = systems.get(name)
+    rng = np.random.default_rng(5)
+    B, H = 1000, 32
+    lo, hi = -3.0, 2.0
+    plan = _planner(d=sysd.n_u, H=H, C=2, lo=lo, hi=hi)
+    x0 = _x0(name, rng)
+    u_norm = rng.uniform(-spread, spread, (B, H, sysd.n_u)).astype(np.float32)
+    u_dev = torch.from_numpy(u_norm).cuda()
+    got = plan.rollout_cost(sysd, x0, u_dev).cpu().numpy()
+    u = unnormalize_np(u_norm, np.full(sysd.n_u, lo), np.full(sysd.n_u, hi)).astype(np.float64)
+    ref = osys.rollout_cost(name, x0, u)
+    if name in EXACT:
+        np.testing.assert_array_equal(got, ref)
+    else:
+        np.testing.assert_allclose(got, ref, rtol=RTOL[name], atol=0)
+
+
+def test_calmpccost_kat5_on_gpu():
+    """SURVEY §8c KAT5 (calMPCCost golden 1154598.1625456358) through the GPU kernel. The kernel
+    unnormalises first, so it is fed u_norm = u/5 with action limits (-5, 5): ((x+1)/2)*10-5."""
+    torch.manual_seed(0)
+    u = torch.randn(1, 32, 1) * 5
+    plan = _planner(d=1, H=32, C=2, lo=-5.0, hi=5.0)
+    red = lambda th: (th - np.pi) ** 2 / -np.pi + np.pi  # noqa: E731
+    x0 = np.array([0.5, 0, 0.9 * np.pi, 0, red(0.9 * np.pi)])
+    u_norm = (u / 5).numpy().astype(np.float32)
+    got = plan.rollout_cost(systems.cartpole_lin5(), x0, torch.from_numpy(u_norm).cuda()).cpu().numpy()
+    ref = osys.rollout_cost("cartpole_lin5", x0, unnormalize_np(u_norm, [-5.0], [5.0]).astype(np.float64))
+    np.testing.assert_array_equal(got, ref)
+    assert osys.rollout_cost("cartpole_lin5", x0, u.double().numpy())[0] == 1154598.1625456358
+    np.testing.assert_allclose(got[0], 1154598.1625456358, rtol=1e-5)
+
+
+def test_unnormalize_global_clip_rule():
+    plan = _planner(d=2, H=16, C=2, lo=-2.0, hi=3.0)
+    rng = np.random.default_rng(1)
+    for spread in (0.99, 1.00005, 1.0002, 1.5):
+        x = rng.uniform(-spread, spread, (37, 16, 2)).astype(np.float32)
+        x[0, 0, 0] = spread
+        got = plan.unnormalize_states(torch.from_numpy(x).cuda()).cpu().numpy()
+        ref = unnormalize_np(x, [-2.0, -2.0], [3.0, 3.0])
+        np.testing.assert_array_equal(got, ref)
+
+
+def test_argmin_nan_and_ties():
+    plan = _planner()
+    c = torch.tensor([5.0, float("nan"), 1.0, 3.0, 1.0, float("nan")], dtype=torch.float64).cuda()
+    assert plan.argmin(c) == (2, 1.0)
+    assert plan.argmin(c, index_offset=100) == (102, 1.0)
+    allnan = torch.full((7,), float("nan"), dtype=torch.float64).cuda()
+    idx, v = plan.argmin(allnan)
+    assert idx == 0 and v == float("inf")
+    big = torch.rand(100003, dtype=torch.float64) + 1
+    big[77777] = 0.5
+    big[99999] = 0.5
+    assert plan.argmin(big.cuda()) == (77777, 0.5)
+
+
+def test_mpc_step_matches_oracle_pipeline():
+    """normalise -> CFG-DDPM sample -> unnormalise -> rollout/cost -> argmin, vs the oracle."""
+    d, H, C, N, B = 1, 32, 5, 25, 128
+    net = make_mlp(d, H, C, seed=9)
+    lo, hi = np.array([-20.0]), np.array([20.0])
+    cmin = np.array([-5, -5, 2, -5, 0], dtype=np.float32)
+    cmax = np.array([5, 5, 4.5, 5, 3.2], dtype=np.float32)
+    plan = DiffusionMPC(NetSpec("mlp", state_dim=d, horizon=H, context_dim=C), net.state_dict(),
+                        n_diffusion_steps=N, action_limits=(lo, hi), context_limits=(cmin, cmax))
+    red = lambda th: (th - np.pi) ** 2 / -np.pi + np.pi  # noqa: E731
+    x0 = np.array([0.3, 0.1, 0.95 * np.pi, -0.2, red(0.95 * np.pi)])
+    noise = torch.randn(N + 1, B, H, d, generator=torch.Generator().manual_seed(1))
+    res = plan.mpc_step(x0, systems.cartpole_lin5(), B, w=0.01, noise=noise)
+    # oracle pipeline
+    from oracle import normalizer as onorm
+    ctx = onorm.normalize(torch.from_numpy(x0)[None], torch.from_numpy(cmin), torch.from_numpy(cmax)).float()
+    x = osam.ddpm_cfg(net, osch.buffers("exponential", N), ctx.expand(B, C), 0.01, B, H, noise=noise)
+    u = onorm.unnormalize(x, torch.from_numpy(lo.astype(np.float32)), torch.from_numpy(hi.astype(np.float32)))
+    cost = osys.rollout_cost("cartpole_lin5", x0, u.double().numpy())
+    i = osys.argmin(cost)
+    gpu_cost = res.costs.cpu().numpy()
+    np.testing.assert_allclose(gpu_cost, cost, rtol=1e-3)
+    if res.best_index != i:  # only acceptable when the two costs tie within the parity bar
+        assert abs(cost[res.best_index] - cost[i]) <= 1e-4 * abs(cost[i])
+    np.testing.assert_allclose(res.u_best, u[res.best_index].numpy(), rtol=1e-4, atol=1e-4 * 20)
+    assert res.u0.shape == (d,)
