@@ -59,3 +59,16 @@ def any_flag(flag_local, group=None):
     t = flag_local.clone()
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return t
+
+
+def select(cost_local, rows_local, argmin, group=None):
+    """The per-control-step exchange: all-gather costs, global argmin on every rank, broadcast the
+    winner's row from its owner. cost_local [B_local] fp64, rows_local [B_local, ...];
+    argmin(costs) -> (global index, cost). Returns (index, cost, row, all costs)."""
+    rank, size = world(group)
+    n_local = cost_local.shape[0]
+    costs = gather_costs(cost_local, group)
+    idx, best = argmin(costs)
+    owner, local = divmod(idx, n_local)
+    row = broadcast_row(rows_local[local if owner == rank else 0], owner, group)
+    return idx, best, row, costs

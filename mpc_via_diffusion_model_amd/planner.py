@@ -304,15 +304,11 @@ class DiffusionMPC:
         if size > 1 and not (sampler == N.MPCD_DDPM_CFG and self.ddpm_final_in_range):
             flag = D.any_flag(self.clip_flag(u_norm), group)
         cost_local = self.rollout_cost(system, x0, u_norm, flag)
-        costs = D.gather_costs(cost_local, group)
-        idx, best = self.argmin(costs)
-        owner, local = divmod(idx, n_samples)
-        row = D.broadcast_row(u_norm[local if owner == rank else 0], owner, group)
-        if flag is None and size == 1:
-            u_best = self.unnormalize_states(row[None], self.clip_flag(u_norm))[0]
-        else:
-            u_best = self.unnormalize_states(row[None], flag if flag is not None else
-                                             torch.zeros(1, dtype=torch.int32, device=self.device))[0]
+        idx, best, row, costs = D.select(cost_local, u_norm, self.argmin, group)
+        if flag is None:
+            # single rank: the flag of the whole batch; provably-zero case on several ranks
+            flag = self.clip_flag(u_norm) if size == 1 else torch.zeros(1, dtype=torch.int32, device=self.device)
+        u_best = self.unnormalize_states(row[None], flag)[0]
         u_host = u_best.cpu().numpy()
         return MPCResult(u0=u_host[0].copy(), u_best=u_host, best_cost=best, best_index=idx, costs=costs,
                          u_norm=u_norm)

@@ -33,13 +33,15 @@ def tables(kind, n_steps):
     ac = torch.cumprod(alpha, axis=0)
     acp = torch.cat([torch.ones(1), ac[:-1]])
     pv = b * (1.0 - acp) / (1.0 - ac)
+    with np.errstate(invalid="ignore"):  # beta > 1 (exponential, some N) -> NaN, as in the reference
+        sq_acp, sq_alpha = np.sqrt(acp.numpy()), np.sqrt(alpha.numpy())
     return {
         "betas": b, "alphas_cumprod": ac, "alphas_cumprod_prev": acp, "sqrt_alphas_cumprod": torch.sqrt(ac),
         "sqrt_one_minus_alphas_cumprod": torch.sqrt(1.0 - ac), "log_one_minus_alphas_cumprod": torch.log(1.0 - ac),
         "sqrt_recip_alphas_cumprod": torch.sqrt(1.0 / ac), "sqrt_recipm1_alphas_cumprod": torch.sqrt(1.0 / ac - 1),
         "posterior_variance": pv, "posterior_log_variance_clipped": torch.log(torch.clamp(pv, min=1e-20)),
-        "posterior_mean_coef1": b * torch.from_numpy(np.sqrt(acp.numpy())) / (1.0 - ac),
-        "posterior_mean_coef2": (1.0 - acp) * torch.from_numpy(np.sqrt(alpha.numpy())) / (1.0 - ac),
+        "posterior_mean_coef1": b * torch.from_numpy(sq_acp) / (1.0 - ac),
+        "posterior_mean_coef2": (1.0 - acp) * torch.from_numpy(sq_alpha) / (1.0 - ac),
     }
 
 

@@ -46,6 +46,7 @@ def buffers(kind, n):
         raise NotImplementedError(kind)
     a = 1.0 - b
     ac = torch.cumprod(a, axis=0)
+    np_err = np.seterr(invalid="ignore")  # beta > 1 (exponential, some N) -> NaN, as in the reference
     acp = torch.cat([torch.ones(1), ac[:-1]])
     pv = b * (1.0 - acp) / (1.0 - ac)
     out = {
@@ -63,4 +64,5 @@ def buffers(kind, n):
         "posterior_mean_coef1": b * torch.from_numpy(np.sqrt(acp.numpy())) / (1.0 - ac),
         "posterior_mean_coef2": (1.0 - acp) * torch.from_numpy(np.sqrt(a.numpy())) / (1.0 - ac),
     }
+    np.seterr(**np_err)
     return out

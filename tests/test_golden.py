@@ -1,0 +1,55 @@
+"""Golden fixtures (tests/golden/*.npz, made by tests/golden/make_golden.py from the KAT-pinned oracle).
+CPU: the oracle still reproduces them bit for bit. GPU: the HIP path matches them to the parity bar."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests.golden import make_golden as G
+
+from ._util import assert_traj_close
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _load(name):
+    return dict(np.load(os.path.join(HERE, name + ".npz")))
+
+
+def _net(c):
+    return G.mlp(c["seed"], c["d"], c["H"], c["C"]) if c["net"] == "mlp" else G.unet(c["seed"], c["d"], c["C"])
+
+
+@pytest.mark.parametrize("name", sorted(G.CASES))
+def test_oracle_reproduces_golden(name, tmp_path, monkeypatch):
+    c = G.CASES[name]
+    fx = _load(name)
+    assert G.blob_sha(_net(c)) == str(fx["weights_sha256"]), "torch init changed: regenerate the fixtures"
+    monkeypatch.setattr(G, "HERE", str(tmp_path))
+    G.make(name, c)
+    new = dict(np.load(os.path.join(tmp_path, name + ".npz")))
+    for k in ("noise", "context", "x0", "chain", "cost", "best"):
+        np.testing.assert_array_equal(new[k], fx[k], err_msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", [n for n in sorted(G.CASES) if G.CASES[n]["net"] == "mlp"])
+def test_gpu_matches_golden(name):
+    from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec, systems
+    c = G.CASES[name]
+    fx = _load(name)
+    net = _net(c)
+    plan = DiffusionMPC(NetSpec(c["net"], c["d"], c["H"], c["C"]), net.state_dict(), variance_schedule=c["schedule"],
+                        n_diffusion_steps=c["N"])
+    noise = torch.from_numpy(fx["noise"])
+    chain = plan.sample_trajectories(torch.from_numpy(fx["context"]), c["B"], c["H"], w=0.01, sample_fn=c["sampler"],
+                                     n_wo_noise=c.get("nwo", 0), clamp_x0=c.get("clamp", False), noise=noise,
+                                     return_chain=True)
+    ref = torch.from_numpy(fx["chain"])
+    assert_traj_close(chain[: ref.shape[0]], ref, what=name)
+    cost = plan.rollout_cost(systems.get(c["system"]), fx["x0"], chain[ref.shape[0] - 1]).cpu().numpy()
+    np.testing.assert_allclose(cost, fx["cost"], rtol=1e-3)
+    idx, _ = plan.argmin(torch.from_numpy(cost).cuda())
+    i = int(fx["best"])
+    assert idx == i or abs(fx["cost"][idx] - fx["cost"][i]) <= 1e-4 * abs(fx["cost"][i])

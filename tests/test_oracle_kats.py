@@ -1,0 +1,144 @@
+"""Pin the oracle to the reference's known-answer tests. CPU only."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import nets, sampler, schedule
+from oracle import systems as osys
+
+REF = "/root/reference"
+CKPT = os.path.join(REF, "trained_models", "cart_pole_84000_test1", "final", "checkpoints",
+                    "ema_model_current_state_dict.pth")
+
+
+def test_kat1_exponential_schedule_values():
+    b = schedule.buffers("exponential", 25)
+    np.testing.assert_allclose(b["betas"][:5].numpy(), [1.0000e-4, 1.46780e-4, 2.15443e-4, 3.16228e-4, 4.64159e-4],
+                               rtol=1e-5)
+    np.testing.assert_allclose(b["betas"][-3:].numpy(), [0.464158, 0.681292, 0.99999917], rtol=1e-6)
+    assert abs(float(b["alphas_cumprod"][-1]) - 4.72e-8) < 1e-10
+    assert abs(float(b["sqrt_recip_alphas_cumprod"][-1]) - 4603) < 1
+    assert abs(float(schedule.buffers("exponential", 50)["alphas_cumprod"][-1]) - 7.70e-10) < 1e-12
+    b100 = schedule.buffers("exponential", 100)
+    assert abs(float(b100["alphas_cumprod"][-1]) - 1.444e-13) < 1e-15
+    assert abs(float(b100["sqrt_recipm1_alphas_cumprod"][-1]) - 2.632e6) < 1e3
+    assert abs(float(schedule.buffers("cosine", 100)["sqrt_recipm1_alphas_cumprod"][-1]) - 2029) < 1
+    assert abs(float(schedule.buffers("cosine", 250)["sqrt_recipm1_alphas_cumprod"][-1]) - 5073) < 1
+    for n in (25, 50, 100):
+        assert abs(float(schedule.buffers("exponential", n)["posterior_log_variance_clipped"][0]) + 46.05) < 0.01
+    # N=250 exponential: beta[-1] = 1.0000001 -> NaN (the hazard bench/config 5 avoids with cosine)
+    b250 = schedule.buffers("exponential", 250)
+    assert float(b250["betas"][-1]) > 1.0
+    assert not torch.isfinite(b250["sqrt_recipm1_alphas_cumprod"]).all()
+
+
+def test_kat1_finite_exponential_n():
+    finite = [n for n in range(2, 401) if all(torch.isfinite(v).all() for v in schedule.buffers("exponential", n).values())]
+    assert finite == [25, 47, 50, 55, 61, 73, 94, 97, 100, 107, 109, 110, 115, 122, 146, 159, 188, 194, 200, 201, 209,
+                      214, 218, 220, 230, 244, 245, 249, 292, 293, 318, 321, 376, 388, 397, 400]
+
+
+def test_kat2_parameter_counts():
+    assert nets.param_count(nets.ConditionedTemporalUnet(state_dim=1, context_dim=5)) == 1000929
+    assert nets.param_count(nets.ConditionedMLPNet(state_dim=2, horizon=32, context_dim=4)) == 121152
+    assert nets.param_count(nets.ConditionedMLPNet(state_dim=2, horizon=16, context_dim=4)) == 119072
+
+
+@pytest.mark.skipif(not os.path.exists(CKPT), reason="reference checkpoint not present")
+def test_kat2_kat3_trained_checkpoint_trace():
+    sd = torch.load(CKPT, map_location="cpu", weights_only=True)
+    n_model = sum(v.numel() for k, v in sd.items() if k.startswith("model."))
+    assert n_model == 1000929 and sum(v.numel() for v in sd.values()) == 1001229
+    net = nets.ConditionedTemporalUnet(state_dim=1, context_dim=5).eval()
+    net.load_state_dict({k[6:]: v for k, v in sd.items() if k.startswith("model.")}, strict=True)
+    bufs = {k: sd[k] for k in schedule.BUFFER_NAMES}
+    mine = schedule.buffers("exponential", 25)
+    assert torch.equal(bufs["betas"], mine["betas"])  # KAT1: recomputed betas equal the checkpoint's
+    torch.manual_seed(0)
+    ctx = torch.rand(1, 5) * 2 - 1
+    np.testing.assert_allclose(ctx[0].numpy(), [-0.0075, 0.5364, -0.8230, -0.7359, -0.3852], atol=5e-5)
+    chain = sampler.ddpm_cfg(net, bufs, ctx, 0.01, 1, 32, n_wo_noise=5, return_chain=True)
+    assert tuple(chain.shape) == (31, 1, 32, 1)
+    np.testing.assert_allclose(chain[-1, 0, :8, 0].numpy(),
+                               [0.9998, 0.9592, 0.9130, 0.8686, 0.8263, 0.7862, 0.7497, 0.7155], atol=5e-5)
+
+
+def _cal_mpc_cost_py(Q, R, P, u, x0, dt):
+    """calMPCCost restated in python/numpy exactly as Cart_Diffusion_inference.py:247-283 evaluates it
+    (scalar indexing: numpy >= 1.24 rejects the reference's ragged object arrays, SURVEY KAT5)."""
+    M_car, m_pole, l_pendul, k, c, G = 4.5, 0.12, 0.14, 0.5, 0.002, 9.81
+    I = (m_pole * l_pendul ** 2) / 3
+    v_1 = (M_car + m_pole) / (I * (M_car + m_pole) + (l_pendul ** 2) * m_pole * M_car)
+    v_2 = (I + (l_pendul ** 2) * m_pole) / (I * (M_car + m_pole) + (l_pendul ** 2) * m_pole * M_car)
+    PI_UNDER_2 = 2 / np.pi
+
+    def f(dt, x, u):
+        xd = np.array([
+            x[1],
+            -k * v_2 * x[1] + ((l_pendul * m_pole) ** 2) * G * v_2 / (I + (l_pendul ** 2) * m_pole) * x[2]
+            - l_pendul * m_pole * c * v_2 / (I + (l_pendul ** 2) * m_pole) * x[3] + v_2 * u,
+            x[3],
+            -l_pendul * m_pole * k * v_1 / (M_car + m_pole) * x[1] + l_pendul * m_pole * G * v_1 * x[2] - c * v_1 * x[3]
+            + l_pendul * m_pole * v_1 / (M_car + m_pole) * u,
+            -PI_UNDER_2 * (x[2] - np.pi) * x[3]])
+        return x + xd * dt
+
+    num_state, num_u, num_hor = x0.shape[0], u.shape[0], u.shape[1]
+    cost = 0
+    for i in range(num_state):
+        cost = cost + Q[i][i] * x0[i] ** 2
+    for i in range(num_u):
+        cost = cost + R * u[i][0][0] ** 2
+    x_cur, u_cur = x0, u[0][0][0]
+    for i in range(1, num_hor - 1):
+        xnext = f(dt, x_cur, u_cur)
+        unext = u[0, i, 0]
+        for j in range(1, num_state):
+            cost = cost + Q[j][j] * xnext[j] ** 2
+        cost = cost + R * unext ** 2
+        u_cur, x_cur = unext, xnext
+    for i in range(num_state):
+        cost = cost + P[i][i] * xnext[i] ** 2
+    return cost
+
+
+def test_kat5_calmpccost_golden():
+    red = lambda th: (th - np.pi) ** 2 / -np.pi + np.pi  # noqa: E731  ThetaToRedTheta
+    x0 = np.array([0.5, 0, 0.9 * np.pi, 0, red(0.9 * np.pi)])
+    torch.manual_seed(0)
+    u = (torch.randn(1, 32, 1) * 5).double().numpy()
+    Q = np.diag([0.01, 0.01, 0, 0.001, 1000.0])
+    assert _cal_mpc_cost_py(Q, 0.1, Q, u, x0, 0.01) == 1154598.1625456358
+    assert osys.rollout_cost("cartpole_lin5", x0, u)[0] == 1154598.1625456358
+
+
+def test_c_oracle_matches_python_calmpccost_random():
+    rng = np.random.default_rng(0)
+    Q = np.diag([0.01, 0.01, 0, 0.001, 1000.0])
+    for _ in range(20):
+        x0 = rng.uniform(-1, 1, 5)
+        H = int(rng.integers(3, 70))
+        u = rng.normal(0, 3, (1, H, 1))
+        assert osys.rollout_cost("cartpole_lin5", x0, u)[0] == _cal_mpc_cost_py(Q, 0.1, Q, u, x0, 0.01)
+
+
+def test_kat6_zoh_matrices():
+    import scipy.linalg as sl
+    from mpc_via_diffusion_model_amd import systems
+    A = np.array([[0, 1, 0, 0], [0, -0.1, 3, 0], [0, 0, 0, 1], [0, -0.5, 30, 0]], float)
+    B = np.array([[0], [2], [0], [5]], float)
+    M = np.zeros((5, 5))
+    M[:4, :4], M[:4, 4:] = A, B
+    E = sl.expm(M * 0.1)
+    np.testing.assert_allclose(np.array(systems.ZOH_A), E[:4, :4], rtol=0, atol=1e-15)
+    np.testing.assert_allclose(np.array(systems.ZOH_B), E[:4, 4], rtol=0, atol=1e-15)
+    np.testing.assert_allclose(E[0, :4], [1, .099495, .015328, .000506], atol=1e-6)
+    np.testing.assert_allclose(E[:4, 4], [.01003, .201522, .025462, .520237], atol=1e-6)
+    assert abs(np.linalg.eigvals(E[:4, :4])).max() == pytest.approx(1.725, abs=1e-3)
+    # the C oracle uses the same A_d/B_d
+    x = np.array([0.3, -0.2, 0.1, 0.05])
+    A_d, B_d = systems.ZOH_A, systems.ZOH_B
+    want = [A_d[i][0] * x[0] + A_d[i][1] * x[1] + A_d[i][2] * x[2] + A_d[i][3] * x[3] + B_d[i] * 0.7 for i in range(4)]
+    np.testing.assert_array_equal(osys.step("cartpole_zoh4", x, [0.7]), want)
