@@ -73,17 +73,28 @@ MPCD_DEV int ntile_of(int wave, int j)
     return MODE == SPLIT ? (wave >> 1) + 2 * j : wave + 4 * j;
 }
 
+// Weight fragments stream in through buffer loads: ONE wave-uniform descriptor per layer (built
+// from readfirstlane'd scalars, T20), the per-lane part is lane*16 in a single VGPR and each
+// (n-tile, k-block) chunk offset is a scalar soffset. A flat/global form kept one 64-bit VGPR
+// address per chunk live across the step loop (hundreds of VGPRs, spills to scratch).
 template <int K, int N, int MODE>
-MPCD_DEV void load_w(WFrag<K, N, MODE> &f, const float *__restrict__ wp, int wave, int lane)
+MPCD_DEV void load_w(WFrag<K, N, MODE> &f, const float *__restrict__ wp, int wave, int lane16)
 {
     constexpr int KB = K / 16, NT = N / 16;
+    const uint64_t a = (uint64_t)wp;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(K * N * sizeof(float)), 0x00020000);
 #pragma unroll
     for (int j = 0; j < WFrag<K, N, MODE>::T; ++j) {
         const int nt = ntile_of<K, N, MODE>(wave, j);
         if (MODE == PAIRED && NT % 4 != 0 && nt >= NT) continue;
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb)
-            f.v[j][kb] = ldg4(wp + ((size_t)(nt * KB + kb) * 64 + lane) * 4);
+        for (int kb = 0; kb < KB; ++kb) {
+            const int soff = __builtin_amdgcn_readfirstlane((nt * KB + kb) * 1024);
+            const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0);
+            f.v[j][kb] = __builtin_bit_cast(f32x4, r);
+        }
     }
 }
 
@@ -287,7 +298,7 @@ struct MlpKernel {
 
     static MPCD_DEV void dump(const MlpSampleArgs &p, const float *buf, int stride, int width, int layer)
     {
-        if (!p.dbg || blockIdx.x != 0) return;
+        if (SMODE != MODE_EPS || !p.dbg || blockIdx.x != 0) return;
         lds_barrier();
         for (int i = threadIdx.x; i < ROWS * width; i += THREADS) {
             const int r = i / width, c = i - r * width;
@@ -302,6 +313,7 @@ struct MlpKernel {
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         const int64_t cand0 = (int64_t)blockIdx.x * CPW;
         constexpr bool has_ctx = CTX;
+        int lane16 = lane * 16;
         const float *wp = p.wpack;
         int wofs = 0;
         auto W = [&](int l) { return wp + wofs + A::woff(l); };
@@ -329,7 +341,7 @@ struct MlpKernel {
         }
 
         WFrag<A::K[0], A::N[0], mode_for<A::N[0]>()> w0;
-        load_w(w0, W(0), wave, lane);
+        load_w(w0, W(0), wave, lane16);
         constexpr int NZT = WFrag<32, D0, PAIRED>::T;
         f32x4 nz[NZT][NB];
         StepPlan sp = p.plan[0];
@@ -338,9 +350,9 @@ struct MlpKernel {
         for (int s = 0; s < p.n_steps; ++s) {
             // Launder the weight base every step: the weights are loop-invariant, and without this
             // LICM hoists all 14 layers' loads out of the step loop (hundreds of live VGPRs -> spills).
-            asm volatile("" : "+s"(wofs));
+            asm volatile("" : "+s"(wofs), "+v"(lane16));
             WFrag<A::K[1], A::N[1], mode_for<A::N[1]>()> w1;
-            load_w(w1, W(1), wave, lane);
+            load_w(w1, W(1), wave, lane16);
             lds_barrier();
             // this step's time projections -> LDS (first read by layer 1, after the next barrier)
             for (int i = threadIdx.x; i < COND_TOTAL / 4; i += THREADS)
@@ -351,78 +363,78 @@ struct MlpKernel {
                                                          cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 32, 0);
             WFrag<A::K[2], A::N[2], mode_for<A::N[2]>()> w2;
-            load_w(w2, W(2), wave, lane);
+            load_w(w2, W(2), wave, lane16);
             lds_barrier();
             hidden_layer<A::K[1], A::N[1], mode_for<A::N[1]>(), EPI_CMISH, NB>(w1, Bs(1), lds + L::T1, L::ST1, false, lds + L::S1, L::SS1, tp, cp,
                                                           0, has_ctx, wave, lane);
             dump(p, lds + L::S1, L::SS1, 32, 1);
             WFrag<A::K[3], A::N[3], mode_for<A::N[3]>()> w3;
-            load_w(w3, W(3), wave, lane);
+            load_w(w3, W(3), wave, lane16);
             lds_barrier();
             hidden_layer<A::K[2], A::N[2], mode_for<A::N[2]>(), EPI_MISH, NB>(w2, Bs(2), lds + L::S1, L::SS1, false, lds + L::T1, L::ST1, tp, cp,
                                                          0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 64, 2);
             WFrag<A::K[4], A::N[4], mode_for<A::N[4]>()> w4;
-            load_w(w4, W(4), wave, lane);
+            load_w(w4, W(4), wave, lane16);
             lds_barrier();
             hidden_layer<A::K[3], A::N[3], mode_for<A::N[3]>(), EPI_CMISH, NB>(w3, Bs(3), lds + L::T1, L::ST1, false, lds + L::C1 + 64, L::SC1,
                                                           tp, cp, 1, has_ctx, wave, lane);
             dump(p, lds + L::C1 + 64, L::SC1, 64, 3);
             WFrag<A::K[5], A::N[5], mode_for<A::N[5]>()> w5;
-            load_w(w5, W(5), wave, lane);
+            load_w(w5, W(5), wave, lane16);
             lds_barrier();
             hidden_layer<A::K[4], A::N[4], mode_for<A::N[4]>(), EPI_MISH, NB>(w4, Bs(4), lds + L::C1 + 64, L::SC1, false, lds + L::T1, L::ST1,
                                                          tp, cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 128, 4);
             WFrag<A::K[6], A::N[6], mode_for<A::N[6]>()> w6;
-            load_w(w6, W(6), wave, lane);
+            load_w(w6, W(6), wave, lane16);
             lds_barrier();
             hidden_layer<A::K[5], A::N[5], mode_for<A::N[5]>(), EPI_CMISH, NB>(w5, Bs(5), lds + L::T1, L::ST1, false, lds + L::C0 + 128,
                                                           L::SC0, tp, cp, 2, has_ctx, wave, lane);
             dump(p, lds + L::C0 + 128, L::SC0, 128, 5);
             WFrag<A::K[7], A::N[7], mode_for<A::N[7]>()> w7;
-            load_w(w7, W(7), wave, lane);
+            load_w(w7, W(7), wave, lane16);
             lds_barrier();
             hidden_layer<A::K[6], A::N[6], mode_for<A::N[6]>(), EPI_MISH, NB>(w6, Bs(6), lds + L::C0 + 128, L::SC0, false, lds + L::T1, L::ST1,
                                                          tp, cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 128, 6);
             WFrag<A::K[8], A::N[8], mode_for<A::N[8]>()> w8;
-            load_w(w8, W(8), wave, lane);
+            load_w(w8, W(8), wave, lane16);
             lds_barrier();
             hidden_layer<A::K[7], A::N[7], mode_for<A::N[7]>(), EPI_CMISH, NB>(w7, Bs(7), lds + L::T1, L::ST1, false, lds + L::C0, L::SC0, tp,
                                                           cp, 3, has_ctx, wave, lane);
             dump(p, lds + L::C0, L::SC0, 128, 7);
             WFrag<A::K[9], A::N[9], mode_for<A::N[9]>()> w9;
-            load_w(w9, W(9), wave, lane);
+            load_w(w9, W(9), wave, lane16);
             lds_barrier();
             hidden_layer<A::K[8], A::N[8], mode_for<A::N[8]>(), EPI_MISH, NB>(w8, Bs(8), lds + L::C0, L::SC0, false, lds + L::T1, L::ST1, tp, cp,
                                                          0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 64, 8);
             WFrag<A::K[10], A::N[10], mode_for<A::N[10]>()> w10;
-            load_w(w10, W(10), wave, lane);
+            load_w(w10, W(10), wave, lane16);
             lds_barrier();
             hidden_layer<A::K[9], A::N[9], mode_for<A::N[9]>(), EPI_CMISH, NB>(w9, Bs(9), lds + L::T1, L::ST1, false, lds + L::C1, L::SC1, tp,
                                                           cp, 4, has_ctx, wave, lane);
             dump(p, lds + L::C1, L::SC1, 64, 9);
             WFrag<A::K[11], A::N[11], mode_for<A::N[11]>()> w11;
-            load_w(w11, W(11), wave, lane);
+            load_w(w11, W(11), wave, lane16);
             lds_barrier();
             hidden_layer<A::K[10], A::N[10], mode_for<A::N[10]>(), EPI_MISH, NB>(w10, Bs(10), lds + L::C1, L::SC1, false, lds + L::T1, L::ST1,
                                                            tp, cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 32, 10);
             WFrag<A::K[12], A::N[12], mode_for<A::N[12]>()> w12;
-            load_w(w12, W(12), wave, lane);
+            load_w(w12, W(12), wave, lane16);
             lds_barrier();
             hidden_layer<A::K[11], A::N[11], mode_for<A::N[11]>(), EPI_CMISH, NB>(w11, Bs(11), lds + L::T1, L::ST1, false, lds + L::S1, L::SS1,
                                                             tp, cp, 5, has_ctx, wave, lane);
             dump(p, lds + L::S1, L::SS1, 32, 11);
             WFrag<A::K[13], A::N[13], PAIRED> w13;
-            load_w(w13, W(13), wave, lane);
+            load_w(w13, W(13), wave, lane16);
             lds_barrier();
             hidden_layer<A::K[12], A::N[12], mode_for<A::N[12]>(), EPI_NONE, NB>(w12, Bs(12), lds + L::S1, L::SS1, false, lds + L::T1, L::ST1,
                                                            tp, cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 32, 12);
-            if (s + 1 < p.n_steps) load_w(w0, W(0), wave, lane);
+            if (s + 1 < p.n_steps) load_w(w0, W(0), wave, lane16);
             const StepPlan cur = sp;
             f32x4 nzc[NZT][NB];
 #pragma unroll
