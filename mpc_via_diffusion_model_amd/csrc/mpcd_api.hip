@@ -581,7 +581,6 @@ int mpcd_eps(mpcd_ctx *c, const float *x, int32_t t, const float *context, int32
     if (cfg && !eps_uncond) return fail(MPCD_EINVAL, "cfg net needs eps_uncond");
     if (d.context_dim > 0 && !context) return fail(MPCD_EINVAL, "net has a context but none given");
     if (t < 0 || t >= c->n_steps) return fail(MPCD_EINVAL, "t out of range");
-    if (d.kind != MPCD_NET_MLP) return fail(MPCD_EUNSUP, "mpcd_eps: UNet forward goes through unet_eps");
     hipStream_t st = static_cast<hipStream_t>(stream_ptr);
     HIP_TRY(hipSetDevice(c->device));
     StepPlan sp{};
@@ -605,6 +604,25 @@ int mpcd_eps(mpcd_ctx *c, const float *x, int32_t t, const float *context, int32
         cproj = c->cproj.as<float>();
         cstride = context_shared ? 0 : c->cond_total;
     }
+    if (d.kind == MPCD_NET_UNET) {
+        UnetSampleArgs u{};
+        u.plan = c->plan.as<StepPlan>();
+        u.tproj = c->tproj.as<float>();
+        u.cproj = cproj;
+        u.cproj_stride = cstride;
+        u.cond_total = c->cond_total;
+        u.batch = batch;
+        u.n_steps = 1;
+        u.mode = cfg ? MODE_EPS : MODE_EPS1;
+        u.x_in = x;
+        u.eps_cond = eps_cond;
+        u.eps_uncond = eps_uncond;
+        if ((rc = c->unet_ws.ensure(unet_workspace_bytes(d, batch, cfg ? 2 : 1)))) return rc;
+        u.workspace = c->unet_ws.p;
+        rc = unet_sample(d, c->unet, u, st);
+        if (rc) return fail(rc, "unet eps: %s", unet_last_error());
+        return MPCD_OK;
+    }
     MlpSampleArgs m{};
     m.wpack = c->wpack.as<float>();
     m.plan = c->plan.as<StepPlan>();
@@ -619,14 +637,6 @@ int mpcd_eps(mpcd_ctx *c, const float *x, int32_t t, const float *context, int32
     m.mode = cfg ? MODE_EPS : MODE_EPS1;
     m.dbg = c->dbg;
     HIP_TRY(launch_mlp_sampler(d.horizon * d.state_dim, cfg ? 2 : 1, m, st));
-    return MPCD_OK;
-}
-
-// Not part of the public header: route per-layer activations of the next mpcd_eps (block 0) to dbg.
-int mpcd_debug_set(mpcd_ctx *c, float *dbg)
-{
-    if (!c) return fail(MPCD_EINVAL, "null ctx");
-    c->dbg = dbg;
     return MPCD_OK;
 }
 

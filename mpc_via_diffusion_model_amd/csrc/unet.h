@@ -4,12 +4,29 @@
 #include <stdint.h>
 
 #include <functional>
+#include <vector>
 
 #include "../../include/mpcd.h"
 #include "internal.h"
 
+// One fused conv launch of the U-Net (see unet.hip for the op list).
+struct ConvLayer {
+    int kind;          // CONV_SAME5 / CONV_DOWN3 / CONV_UP4 / CONV_PW1
+    int cin, cout;     // total input channels (a + b concat), output channels
+    int coutp;         // cout padded to a multiple of 16 (MFMA n-tiles)
+    int cinp;          // cin padded to a multiple of 4 (first layer: d -> 4/8)
+    int kpad;          // packed K per parity, multiple of 16
+    const float *w;    // packed A operand (device), [parities][cout/16][kpad/16][64][4]
+    const float *bias; // [cout]
+    const float *gn_w, *gn_b;  // GroupNorm affine or null
+    int groups;
+    int cond_off;      // column of this block in tproj/cproj, -1 = none
+};
+
 struct UnetWeights {
     bool ready = false;
+    int n_layers = 0;
+    std::vector<ConvLayer> layers;  // in execution order (see unet.hip build_plan)
 };
 
 struct UnetSampleArgs {
@@ -30,6 +47,8 @@ struct UnetSampleArgs {
     int32_t clamp_x0;
     float wp1, wf;
     void *workspace;
+    float *eps_cond, *eps_uncond;  // MODE_EPS / MODE_EPS1 outputs
+    const float *x_in;             // MODE_EPS / MODE_EPS1 input
 };
 
 using TensorLookup = std::function<const float *(const char *)>;

@@ -34,7 +34,7 @@ def test_oracle_reproduces_golden(name, tmp_path, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", [n for n in sorted(G.CASES) if G.CASES[n]["net"] == "mlp"])
+@pytest.mark.parametrize("name", sorted(G.CASES))
 def test_gpu_matches_golden(name):
     from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec, systems
     c = G.CASES[name]

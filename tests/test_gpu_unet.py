@@ -1,0 +1,133 @@
+"""GPU parity: 1D temporal U-Net (ConditionedTemporalUnet / TemporalUnet) forward, CFG-DDPM, CFG-DDIM,
+reference DDIM, and the trained cart-pole checkpoint, through the C ABI."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec
+from oracle import sampler as osam
+from oracle import schedule as osch
+
+from ._util import assert_traj_close, make_unet, oracle_sensitivity
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _planner(net, d, H, C, N=25, kind="exponential", cfg=True, mults=(1, 2, 4)):
+    spec = NetSpec("unet", state_dim=d, horizon=H, context_dim=C, cfg=cfg, dim_mults=mults)
+    return DiffusionMPC(spec, net.state_dict(), variance_schedule=kind, n_diffusion_steps=N)
+
+
+def _close_eps(got, ref, what):
+    err = float((got.cpu() - ref).abs().max())
+    scale = float(ref.abs().max())
+    assert err <= 2e-5 * max(scale, 1.0), f"{what}: eps max err {err:.3e} (|eps| max {scale:.2f})"
+
+
+@pytest.mark.parametrize("d,H,C,B", [(1, 32, 5, 24), (2, 16, 4, 16), (1, 64, 5, 6), (7, 128, 20, 3), (4, 64, 12, 5)])
+def test_cfg_unet_forward_matches_oracle(d, H, C, B):
+    net = make_unet(d, C, seed=d + H)
+    plan = _planner(net, d, H, C, N=50)
+    g = torch.Generator().manual_seed(H)
+    x = torch.randn(B, H, d, generator=g)
+    for shared in (True, False):
+        ctx = torch.rand(1 if shared else B, C, generator=g) * 2 - 1
+        for t in (0, 31, 49):
+            ec, eu = plan.eps(x, t, ctx)
+            tt = torch.full((B,), t, dtype=torch.long)
+            with torch.no_grad():
+                rc = net(x, tt, ctx.expand(B, C), torch.zeros(B, 1))
+                ru = net(x, tt, ctx.expand(B, C), torch.ones(B, 1))
+            _close_eps(ec, rc, f"cond d={d} H={H} t={t}")
+            _close_eps(eu, ru, f"uncond d={d} H={H} t={t}")
+
+
+@pytest.mark.parametrize("C,mults,H", [(0, (1, 2, 4), 32), (3, (1, 2, 4, 8), 64)])
+def test_temporal_unet_forward_matches_oracle(C, mults, H):
+    d, B = 2, 8
+    net = make_unet(d, C, mults=mults, seed=4, cfg=False)
+    plan = _planner(net, d, H, C, N=100, cfg=False, mults=mults)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(B, H, d, generator=g)
+    ctx = torch.rand(B, C, generator=g) * 2 - 1 if C else None
+    for t in (0, 57, 99):
+        e, none = plan.eps(x, t, ctx)
+        assert none is None
+        with torch.no_grad():
+            r = net(x, torch.full((B,), t, dtype=torch.long), ctx)
+        _close_eps(e, r, f"TemporalUnet C={C} t={t}")
+
+
+@pytest.mark.parametrize("B,H,d,C,N,nwo", [(8, 64, 1, 5, 25, 0), (5, 32, 1, 5, 25, 5), (4, 64, 4, 12, 50, 0)])
+def test_cfg_ddpm_unet_matches_oracle(B, H, d, C, N, nwo):
+    """cfg 4 (cart-pole, H=64) / cfg 5 (quadrotor, d=4, C=12) shapes at oracle-sized batches."""
+    net = make_unet(d, C, seed=3)
+    plan = _planner(net, d, H, C, N=N)
+    g = torch.Generator().manual_seed(9)
+    ctx = torch.rand(1, C, generator=g) * 2 - 1
+    noise = torch.randn(N + nwo + 1, B, H, d, generator=g)
+    ref = osam.ddpm_cfg(net, osch.buffers("exponential", N), ctx.expand(B, C), 0.01, B, H, nwo, noise=noise,
+                        return_chain=True)
+    got = plan.run_CFG(ctx, None, 0.01, n_samples=B, horizon=H, return_chain=True, noise=noise,
+                       n_diffusion_steps_without_noise=nwo)
+    assert_traj_close(got, ref, what=f"unet ddpm H={H} d={d}")
+
+
+def test_cfg_ddim_unet_pendulum_shape():
+    """cfg 3 shape (pendulum: d=1, C=2, H=32, N=100) with the build-defined CFG-DDIM."""
+    B, H, d, C, N = 6, 32, 1, 2, 100
+    net = make_unet(d, C, seed=8)
+    plan = _planner(net, d, H, C, N=N)
+    g = torch.Generator().manual_seed(2)
+    ctx = torch.rand(1, C, generator=g) * 2 - 1
+    S = len(osam.ddim_grid(N))
+    noise = torch.randn(S + 1, B, H, d, generator=g)
+    ref, spread = oracle_sensitivity(lambda: osam.ddim_cfg(net, osch.buffers("exponential", N), ctx.expand(B, C), 0.01,
+                                                           B, H, noise=noise, return_chain=True))
+    got = plan.sample_trajectories(ctx, B, H, sample_fn="ddim_cfg", noise=noise, return_chain=True)
+    assert_traj_close(got[: ref.shape[0]], ref, abs_elem=max(1e-4, 4 * spread), what="unet ddim_cfg")
+
+
+def test_reference_ddim_temporal_unet():
+    """Reference ddim_sample (3-arg TemporalUnet, conditioning None), SURVEY §8a A8 parity anchor."""
+    B, H, d, N = 6, 32, 1, 100
+    net = make_unet(d, 0, seed=5, cfg=False)
+    plan = _planner(net, d, H, 0, N=N, cfg=False)
+    g = torch.Generator().manual_seed(3)
+    S = len(osam.ddim_grid(N))
+    noise = torch.randn(S + 1, B, H, d, generator=g)
+    ref, spread = oracle_sensitivity(lambda: osam.ddim(net, osch.buffers("exponential", N), B, H, noise=noise,
+                                                       return_chain=True))
+    got = plan.sample_trajectories(None, B, H, sample_fn="ddim", noise=noise, return_chain=True)
+    assert_traj_close(got[: ref.shape[0]], ref, abs_elem=max(1e-4, 4 * spread), what="ddim TemporalUnet")
+
+
+def test_kat3_trained_checkpoint_on_gpu():
+    """trained cart_pole_84000_test1 EMA weights + the checkpoint's own schedule
+    buffers; torch.manual_seed(0) context/noise stream; final u[0:8] to 4 decimals."""
+    from safetensors.torch import load_file
+    sd = load_file(os.path.join(HERE, "golden", "cart_pole_84000_test1_ema.safetensors"))
+    plan = DiffusionMPC.from_state_dict(sd, NetSpec("unet", state_dim=1, horizon=32, context_dim=5))
+    torch.manual_seed(0)
+    ctx = torch.rand(1, 5) * 2 - 1
+    noise = torch.stack([torch.randn(1, 32, 1) for _ in range(31)])  # x_T + 30 randn_like draws
+    chain = plan.run_CFG(ctx, None, 0.01, n_samples=1, horizon=32, return_chain=True, noise=noise,
+                         n_diffusion_steps_without_noise=5)
+    assert tuple(chain.shape) == (31, 1, 32, 1)
+    np.testing.assert_allclose(chain[-1, 0, :8, 0].cpu().numpy(),
+                               [0.9998, 0.9592, 0.9130, 0.8686, 0.8263, 0.7862, 0.7497, 0.7155], atol=5e-5)
+
+
+def test_unet_philox_shard_invariance():
+    B, H, d, C, N = 40, 32, 1, 5, 25
+    net = make_unet(d, C, seed=1)
+    plan = _planner(net, d, H, C, N=N)
+    ctx = torch.rand(1, C) * 2 - 1
+    full = plan.sample_trajectories(ctx, B, H, seed=5)
+    a = plan.sample_trajectories(ctx, 16, H, seed=5, global_offset=0)
+    b = plan.sample_trajectories(ctx, B - 16, H, seed=5, global_offset=16)
+    assert torch.equal(full, torch.cat([a, b]))
+    assert torch.isfinite(full).all() and float(full.abs().max()) <= 1.0 + 1e-6
