@@ -39,13 +39,13 @@ __global__ __launch_bounds__(128) void time_prologue_kernel(const StepPlan *plan
     {
         double acc = 0.0;
         for (int k = 0; k < TDIM; ++k) acc += (double)w1[tid * TDIM + k] * (double)emb[k];
-        hid[tid] = mish((float)(acc + (double)b1[tid]));
+        hid[tid] = mish_precise((float)(acc + (double)b1[tid]));
     }
     __syncthreads();
     if (tid < TDIM) {
         double acc = 0.0;
         for (int k = 0; k < THID; ++k) acc += (double)w2[tid * THID + k] * (double)hid[k];
-        mt[tid] = mish((float)(acc + (double)b2[tid]));  // cond_mlp's leading Mish on the time part of c_emb
+        mt[tid] = mish_precise((float)(acc + (double)b2[tid]));  // cond_mlp's leading Mish on the time part of c_emb
     }
     __syncthreads();
     for (int l = 0; l < n_layers; ++l) {
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void ctx_prologue_kernel(const float *ctx, int
     const CondLayer L = layers[l];
     const int n = col - L.off;
     double acc = 0.0;
-    for (int k = 0; k < ctx_dim; ++k) acc += (double)L.W[(size_t)n * cond_dim + TDIM + k] * (double)mish(ctx[row * ctx_dim + k]);
+    for (int k = 0; k < ctx_dim; ++k) acc += (double)L.W[(size_t)n * cond_dim + TDIM + k] * (double)mish_precise(ctx[row * ctx_dim + k]);
     cproj[i] = (float)acc;
 }
 

@@ -35,6 +35,8 @@ struct Arch {
     static constexpr int N[NLAYER] = {32, 32, 64, 64, 128, 128, 128, 128, 64, 64, 32, 32, 32, D0};
     static constexpr int woff(int l) { return l == 0 ? 0 : woff(l - 1) + K[l - 1] * N[l - 1] + N[l - 1]; }
     static constexpr int total() { return woff(NLAYER); }
+    static constexpr int boff(int l) { return l == 0 ? 0 : boff(l - 1) + N[l - 1]; }  // biases staged in LDS
+    static constexpr int btotal() { return boff(NLAYER); }
 };
 
 // cond block j (0..5) -> column offset in the 448-wide tables
@@ -52,7 +54,8 @@ struct Lds {
     static constexpr int C1 = S1 + ROWS * SS1;
     static constexpr int C0 = C1 + ROWS * SC1;
     static constexpr int TP = C0 + ROWS * SC0;     // this step's tproj [448]
-    static constexpr int CP = TP + COND_TOTAL;     // per-candidate cproj [CPW][448]
+    static constexpr int BI = TP + COND_TOTAL;     // all 14 biases
+    static constexpr int CP = BI + Arch<D0>::btotal();  // per-candidate cproj [CPW][448]
     static constexpr int total(bool ctx) { return CP + (ctx ? CPW * COND_TOTAL : 0); }
 };
 
@@ -147,7 +150,7 @@ MPCD_DEV void hidden_layer(const WFrag<K, N, MODE> &f, const float *__restrict__
         const int nt = ntile_of<K, N, MODE>(wave, j);
         if (MODE == PAIRED && NT % 4 != 0 && nt >= NT) continue;
         const int n = nt * 16 + 4 * q;
-        const f32x4 b4 = ldg4(bias + n);
+        const f32x4 b4 = *reinterpret_cast<const f32x4 *>(bias + n);
         f32x4 tc = f32x4{0.f, 0.f, 0.f, 0.f};
         if (EPI == EPI_CMISH) tc = *reinterpret_cast<const f32x4 *>(tp + cond_off(cond_j) + n);
 #pragma unroll
@@ -218,7 +221,7 @@ struct MlpKernel {
             const int nt = wave + 4 * j;
             if (NT % 4 != 0 && nt >= NT) continue;
             const int n = nt * 16 + 4 * q;
-            const f32x4 b4 = ldg4(bias + n);
+            const f32x4 b4 = *reinterpret_cast<const f32x4 *>(bias + n);
 #pragma unroll
             for (int g = 0; g < (NB == 2 ? 1 : 2); ++g) {
                 // NB == 2: one candidate per lane column, eps_c = tile 0, eps_u = tile 1
@@ -317,8 +320,11 @@ struct MlpKernel {
         const float *wp = p.wpack;
         int wofs = 0;
         auto W = [&](int l) { return wp + wofs + A::woff(l); };
-        auto Bs = [&](int l) { return wp + wofs + A::woff(l) + A::K[l] * A::N[l]; };
+        auto Bs = [&](int l) { return lds + L::BI + A::boff(l); };
 
+        // biases of every layer -> LDS (read in each epilogue instead of a global round trip)
+        for (int l = 0; l < NLAYER; ++l)
+            for (int i = threadIdx.x; i < A::N[l]; i += THREADS) lds[L::BI + A::boff(l) + i] = wp[A::woff(l) + A::K[l] * A::N[l] + i];
         // per-candidate context projections (constant over the denoise loop)
         if (has_ctx) {
             for (int i = threadIdx.x; i < CPW * COND_TOTAL; i += THREADS) {

@@ -1,0 +1,31 @@
+"""Quick U-Net throughput probe: one sample_trajectories call at a BASELINE shape (per-GPU shard)."""
+import sys, os, time, argparse
+import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec
+from oracle import nets
+ap = argparse.ArgumentParser()
+ap.add_argument("--B", type=int, default=16384)
+ap.add_argument("--H", type=int, default=32)
+ap.add_argument("--d", type=int, default=1)
+ap.add_argument("--C", type=int, default=2)
+ap.add_argument("--N", type=int, default=100)
+ap.add_argument("--steps", type=int, default=10, help="DDIM sampling steps (network evaluations)")
+ap.add_argument("--reps", type=int, default=2)
+a = ap.parse_args()
+torch.manual_seed(0)
+net = nets.ConditionedTemporalUnet(state_dim=a.d, context_dim=a.C)
+plan = DiffusionMPC(NetSpec("unet", a.d, a.H, a.C), net.state_dict(), n_diffusion_steps=a.N)
+ctx = torch.rand(1, a.C) * 2 - 1
+plan.sample_trajectories(ctx, a.B, a.H, sample_fn="ddim_cfg", ddim_steps=2)
+torch.cuda.synchronize()
+for _ in range(a.reps):
+    t0 = time.perf_counter()
+    x = plan.sample_trajectories(ctx, a.B, a.H, sample_fn="ddim_cfg", ddim_steps=a.steps)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    evals = a.steps + 1
+    mac = {32: 9122560, 64: 18209152}.get(a.H, 0) + 896 * (a.C - 5)
+    fl = a.B * evals * 2 * 2 * mac
+    print(f"B={a.B} H={a.H}: {el*1e3:.1f} ms for {evals} CFG net evals -> {el/evals*1e3:.2f} ms/eval, "
+          f"{fl/el/1e12:.1f} TFLOP/s, {a.B/el*evals/101:.0f} cand/s at 101 evals")
