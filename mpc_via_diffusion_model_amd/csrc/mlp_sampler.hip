@@ -33,9 +33,18 @@ template <int D0>
 struct Arch {
     static constexpr int K[NLAYER] = {D0, 32, 32, 64, 64, 128, 128, 128, 256, 64, 128, 32, 32, 32};
     static constexpr int N[NLAYER] = {32, 32, 64, 64, 128, 128, 128, 128, 64, 64, 32, 32, 32, D0};
-    static constexpr int woff(int l) { return l == 0 ? 0 : woff(l - 1) + K[l - 1] * N[l - 1] + N[l - 1]; }
+    // Loop form (not recursion) so the device inliner folds every call to a constant.
+    __host__ __device__ static constexpr int woff(int l) {
+        int o = 0;
+        for (int i = 0; i < l; ++i) o += K[i] * N[i] + N[i];
+        return o;
+    }
     static constexpr int total() { return woff(NLAYER); }
-    static constexpr int boff(int l) { return l == 0 ? 0 : boff(l - 1) + N[l - 1]; }  // biases staged in LDS
+    __host__ __device__ static constexpr int boff(int l) {  // biases staged in LDS
+        int o = 0;
+        for (int i = 0; i < l; ++i) o += N[i];
+        return o;
+    }
     static constexpr int btotal() { return boff(NLAYER); }
 };
 
