@@ -10,7 +10,8 @@ import os
 import torch  # noqa: F401  (load torch's HIP runtime before libmpcd.so)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmpcd.so")
+# MPCD_LIB: load an experiment build (build.py variant) instead of the product library
+LIB_PATH = os.environ.get("MPCD_LIB") or os.path.join(_HERE, "libmpcd.so")
 
 MPCD_NET_MLP, MPCD_NET_UNET = 1, 2
 MPCD_F32, MPCD_F16 = 0, 1

@@ -35,17 +35,24 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, variant=None, defines=()):
+    """variant: build an experiment copy (libmpcd_<variant>.so, objects in _build_<variant>/) with
+    extra -D defines; load it with MPCD_LIB=<path>. The default build is the product library."""
     cc = hipcc()
-    os.makedirs(OBJ, exist_ok=True)
+    out, obj, flags = OUT, OBJ, list(FLAGS)
+    if variant:
+        out = os.path.join(PKG, f"libmpcd_{variant}.so")
+        obj = OBJ + "_" + variant
+        flags += [f"-D{d}" for d in defines]
+    os.makedirs(obj, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     headers.append(os.path.join(os.path.dirname(PKG), "include", "mpcd.h"))
     jobs = []
     for src in SOURCES:
         s = os.path.join(CSRC, src)
-        o = os.path.join(OBJ, src.replace(".hip", ".o"))
+        o = os.path.join(obj, src.replace(".hip", ".o"))
         if force or _stale(o, [s] + headers):
-            jobs.append([cc] + FLAGS + ["-c", s, "-o", o])
+            jobs.append([cc] + flags + ["-c", s, "-o", o])
 
     def run(cmd):
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -56,11 +63,13 @@ def build(force=False, verbose=False):
 
     with cf.ThreadPoolExecutor(max_workers=min(len(jobs), 8) or 1) as ex:
         list(ex.map(run, jobs))
-    objs = [os.path.join(OBJ, s.replace(".hip", ".o")) for s in SOURCES]
-    if force or jobs or _stale(OUT, objs):
-        run([cc, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", OUT] + objs)
-    return OUT
+    objs = [os.path.join(obj, s.replace(".hip", ".o")) for s in SOURCES]
+    if force or jobs or _stale(out, objs):
+        run([cc, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", out] + objs)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    args = [a for a in sys.argv[1:] if a != "--force"]
+    variant = args[0] if args else None
+    print(build(force="--force" in sys.argv, verbose=True, variant=variant, defines=args[1:]))

@@ -26,6 +26,7 @@ constexpr int ROWS = 32;
 constexpr int THREADS = 256;
 constexpr int NLAYER = 14;
 constexpr int COND_TOTAL = 448;  // 32+64+128+128+64+32
+constexpr int CP_STRIDE = COND_TOTAL + 4;  // LDS cproj row stride (448 = 0 mod 64 banks: 16-way conflict)
 enum { EPI_NONE = 0, EPI_MISH = 1, EPI_CMISH = 2 };
 enum { SPLIT = 0, PAIRED = 1 };
 
@@ -65,7 +66,7 @@ struct Lds {
     static constexpr int TP = C0 + ROWS * SC0;     // this step's tproj [448]
     static constexpr int BI = TP + COND_TOTAL;     // all 14 biases
     static constexpr int CP = BI + Arch<D0>::btotal();  // per-candidate cproj [CPW][448]
-    static constexpr int total(bool ctx) { return CP + (ctx ? CPW * COND_TOTAL : 0); }
+    static constexpr int total(bool ctx) { return CP + (ctx ? CPW * CP_STRIDE : 0); }
 };
 
 template <int N>
@@ -110,6 +111,20 @@ MPCD_DEV void load_w(WFrag<K, N, MODE> &f, const float *__restrict__ wp, int wav
     }
 }
 
+// Two independent 16-k chains, issued alternately: a v_mfma_f32_16x16x4_f32 whose C operand is the
+// previous MFMA's result waits 40 cycles instead of issuing at the 32-cycle pipe rate.
+MPCD_DEV void mfma4x2(const f32x4 &wa, const f32x4 &aa, f32x4 &acca, const f32x4 &wb, const f32x4 &ab, f32x4 &accb)
+{
+    acca = __builtin_amdgcn_mfma_f32_16x16x4f32(wa.x, aa.x, acca, 0, 0, 0);
+    accb = __builtin_amdgcn_mfma_f32_16x16x4f32(wb.x, ab.x, accb, 0, 0, 0);
+    acca = __builtin_amdgcn_mfma_f32_16x16x4f32(wa.y, aa.y, acca, 0, 0, 0);
+    accb = __builtin_amdgcn_mfma_f32_16x16x4f32(wb.y, ab.y, accb, 0, 0, 0);
+    acca = __builtin_amdgcn_mfma_f32_16x16x4f32(wa.z, aa.z, acca, 0, 0, 0);
+    accb = __builtin_amdgcn_mfma_f32_16x16x4f32(wb.z, ab.z, accb, 0, 0, 0);
+    acca = __builtin_amdgcn_mfma_f32_16x16x4f32(wa.w, aa.w, acca, 0, 0, 0);
+    accb = __builtin_amdgcn_mfma_f32_16x16x4f32(wb.w, ab.w, accb, 0, 0, 0);
+}
+
 MPCD_DEV f32x4 mfma4(const f32x4 &w, const f32x4 &a, f32x4 acc)
 {
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, a.x, acc, 0, 0, 0);
@@ -119,10 +134,28 @@ MPCD_DEV f32x4 mfma4(const f32x4 &w, const f32x4 &a, f32x4 acc)
     return acc;
 }
 
+// Ask the scheduler for NM x {1 MFMA, NV VALU}: the previous group's epilogue rides in the MFMA
+// issue gaps (32 cycles per v_mfma_f32_16x16x4_f32, ~24 of them free for VALU).
+template <int NM, int NV>
+MPCD_DEV void interleave()
+{
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+    }
+}
+
 // Hidden layer. SPLIT (N = 32): wave w -> column tile (w & 1), n-tiles (w >> 1) + 2j.
 // PAIRED (N >= 64): wave w -> n-tiles w + 4j for BOTH column tiles, so each weight register feeds
 // two MFMAs and a wave holds only a quarter of the layer's weights.
 // in_shared: both column tiles read rows 0..15 (layer 0 with CFG: both branches see the same x).
+//
+// Schedule: the wave's output tiles form G groups of two independent accumulation chains (two
+// column tiles of one n-tile when T = 2, else the even / odd k-blocks of one tile, summed at the
+// end), so the MFMA pipe never waits on a dependent chain; group g's MFMAs are issued together
+// with group g-1's epilogue (bias, cond, Mish, ds_write), leaving only the last group's epilogue
+// exposed before the barrier. Activations, bias and cond operands are read from LDS up front.
 template <int K, int N, int MODE, int EPI, int NB>
 MPCD_DEV void hidden_layer(const WFrag<K, N, MODE> &f, const float *__restrict__ bias, const float *in, int in_stride,
                            bool in_shared, float *out, int out_stride, const float *tp, const float *cp, int cond_j,
@@ -130,69 +163,94 @@ MPCD_DEV void hidden_layer(const WFrag<K, N, MODE> &f, const float *__restrict__
 {
     constexpr int T = WFrag<K, N, MODE>::T, KB = K / 16, NT = N / 16;
     constexpr int NCT = MODE == SPLIT ? 1 : 2;
+    static_assert(MODE == SPLIT || NT % 4 == 0, "PAIRED hidden layers need N % 64 == 0");
+    static_assert(KB % 2 == 0, "even / odd k-block chains need K % 32 == 0");
+    static_assert(T <= 2 && (T == 1 || NCT == 2), "group layout");
+    constexpr bool BYJ = T == 2;        // group = n-tile j, chains = the two column tiles
+    constexpr int G = BYJ ? T : NCT;    // else group = column tile, chains = even / odd k-blocks
     const int col = lane & 15, q = lane >> 4;
-    const float *arow[NCT];
+
+    f32x4 a[NCT][KB];
 #pragma unroll
     for (int c = 0; c < NCT; ++c) {
         const int ct = MODE == SPLIT ? (wave & 1) : c;
-        arow[c] = in + (size_t)((in_shared ? 0 : ct * 16) + col) * in_stride + 4 * q;
+        const float *arow = in + (size_t)((in_shared ? 0 : ct * 16) + col) * in_stride + 4 * q;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) a[c][kb] = *reinterpret_cast<const f32x4 *>(arow + kb * 16);
     }
-    f32x4 acc[T][NCT];
-#pragma unroll
-    for (int j = 0; j < T; ++j)
-#pragma unroll
-        for (int c = 0; c < NCT; ++c) acc[j][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-        f32x4 a[NCT];
-#pragma unroll
-        for (int c = 0; c < NCT; ++c) a[c] = *reinterpret_cast<const f32x4 *>(arow[c] + kb * 16);
-#pragma unroll
-        for (int j = 0; j < T; ++j) {
-            if (MODE == PAIRED && NT % 4 != 0 && ntile_of<K, N, MODE>(wave, j) >= NT) continue;
-#pragma unroll
-            for (int c = 0; c < NCT; ++c) acc[j][c] = mfma4(f.v[j][kb], a[c], acc[j][c]);
-        }
-    }
+    f32x4 b4[T], cv[T][NCT];
 #pragma unroll
     for (int j = 0; j < T; ++j) {
-        const int nt = ntile_of<K, N, MODE>(wave, j);
-        if (MODE == PAIRED && NT % 4 != 0 && nt >= NT) continue;
-        const int n = nt * 16 + 4 * q;
-        const f32x4 b4 = *reinterpret_cast<const f32x4 *>(bias + n);
-        f32x4 tc = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (EPI == EPI_CMISH) tc = *reinterpret_cast<const f32x4 *>(tp + cond_off(cond_j) + n);
+        const int n = ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q;
+        b4[j] = *reinterpret_cast<const f32x4 *>(bias + n);
+        if (EPI != EPI_CMISH) continue;
+        const f32x4 tc = *reinterpret_cast<const f32x4 *>(tp + cond_off(cond_j) + n);
 #pragma unroll
         for (int c = 0; c < NCT; ++c) {
+            // NB == 2: column tile = branch (0: context, 1: masked -> time part only); NB == 1: all unmasked.
+            // Branch-free select (the masked rows take tc exactly): a wave-uniform branch around this
+            // LDS load let the masked rows consume a stale .w register (seen on gfx950 / ROCm 7.2).
             const int ct = MODE == SPLIT ? (wave & 1) : c;
-            const int row = ct * 16 + col;
-            f32x4 v = acc[j][c] + b4;
-            if (EPI == EPI_CMISH) {
-                // NB == 2: column tile = branch (0: context, 1: masked -> time part only); NB == 1: all unmasked.
-                // Branch-free select (the masked rows take tc exactly): a wave-uniform branch around this
-                // LDS load let the masked rows consume a stale .w register (seen on gfx950 / ROCm 7.2).
-                f32x4 cv = tc;
-                if (has_ctx) {
-                    const int cand = NB == 2 ? col : row;
-                    const f32x4 cpv = *reinterpret_cast<const f32x4 *>(cp + cand * COND_TOTAL + cond_off(cond_j) + n);
-                    const f32x4 sum = tc + cpv;
-                    const bool take = NB == 1 || ct == 0;
-                    cv.x = take ? sum.x : tc.x;
-                    cv.y = take ? sum.y : tc.y;
-                    cv.z = take ? sum.z : tc.z;
-                    cv.w = take ? sum.w : tc.w;
-                }
-                v = v + cv;
+            cv[j][c] = tc;
+            if (has_ctx) {
+                const int cand = NB == 2 ? col : ct * 16 + col;
+                const f32x4 cpv = *reinterpret_cast<const f32x4 *>(cp + cand * CP_STRIDE + cond_off(cond_j) + n);
+                const f32x4 sum = tc + cpv;
+                const bool take = NB == 1 || ct == 0;
+                cv[j][c].x = take ? sum.x : tc.x;
+                cv[j][c].y = take ? sum.y : tc.y;
+                cv[j][c].z = take ? sum.z : tc.z;
+                cv[j][c].w = take ? sum.w : tc.w;
             }
-            if (EPI != EPI_NONE) {
-                v.x = mish(v.x);
-                v.y = mish(v.y);
-                v.z = mish(v.z);
-                v.w = mish(v.w);
-            }
-            *reinterpret_cast<f32x4 *>(out + (size_t)row * out_stride + n) = v;
         }
     }
+
+    f32x4 acc[G][2];
+    auto chain = [&](int g) {
+        acc[g][0] = acc[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (BYJ) {
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) mfma4x2(f.v[g][kb], a[0][kb], acc[g][0], f.v[g][kb], a[1][kb], acc[g][1]);
+        } else {
+#pragma unroll
+            for (int kb = 0; kb < KB; kb += 2)
+                mfma4x2(f.v[0][kb], a[g][kb], acc[g][0], f.v[0][kb + 1], a[g][kb + 1], acc[g][1]);
+        }
+    };
+    auto store = [&](int j, int c, f32x4 v) {
+        const int ct = MODE == SPLIT ? (wave & 1) : c;
+        const int n = ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q;
+        v = v + b4[j];
+        if (EPI == EPI_CMISH) v = v + cv[j][c];
+        if (EPI != EPI_NONE) {
+            v.x = mish(v.x);
+            v.y = mish(v.y);
+            v.z = mish(v.z);
+            v.w = mish(v.w);
+        }
+        *reinterpret_cast<f32x4 *>(out + (size_t)(ct * 16 + col) * out_stride + n) = v;
+    };
+    auto epi = [&](int g) {
+        if (BYJ) {
+#pragma unroll
+            for (int c = 0; c < NCT; ++c) store(g, c, acc[g][c]);
+        } else {
+            store(0, g, acc[g][0] + acc[g][1]);
+        }
+    };
+    // MFMAs per group and the epilogue's VALU per MFMA slot (~16 VALU per output element incl. Mish)
+    constexpr int NM = BYJ ? KB * 4 * NCT : KB * 4;
+    constexpr int EPI_VALU = (BYJ ? NCT : 1) * 4 * (EPI == EPI_NONE ? 2 : 16);
+    constexpr int NV = (EPI_VALU + NM - 1) / NM;
+    chain(0);
+#pragma unroll
+    for (int g = 1; g < G; ++g) {
+        __builtin_amdgcn_sched_barrier(0);
+        chain(g);
+        epi(g - 1);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    epi(G - 1);
 }
 
 template <int D0, int SMODE, bool CTX>
@@ -213,16 +271,15 @@ struct MlpKernel {
         f32x4 acc[T][2];
 #pragma unroll
         for (int j = 0; j < T; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const float *arow0 = lds + L::T1 + (size_t)col * L::ST1 + 4 * q;
+        const float *arow1 = arow0 + 16 * L::ST1;
 #pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-            const float *arow = lds + L::T1 + (size_t)(ct * 16 + col) * L::ST1 + 4 * q;
+        for (int kb = 0; kb < 2; ++kb) {
+            const f32x4 a0 = *reinterpret_cast<const f32x4 *>(arow0 + kb * 16);
+            const f32x4 a1 = *reinterpret_cast<const f32x4 *>(arow1 + kb * 16);
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb) {
-                const f32x4 a = *reinterpret_cast<const f32x4 *>(arow + kb * 16);
-#pragma unroll
-                for (int j = 0; j < T; ++j)
-                    if (NT % 4 == 0 || wave + 4 * j < NT) acc[j][ct] = mfma4(f.v[j][kb], a, acc[j][ct]);
-            }
+            for (int j = 0; j < T; ++j)
+                if (NT % 4 == 0 || wave + 4 * j < NT) mfma4x2(f.v[j][kb], a0, acc[j][0], f.v[j][kb], a1, acc[j][1]);
         }
         const bool last = s == p.n_steps - 1;
 #pragma unroll
@@ -339,7 +396,7 @@ struct MlpKernel {
             for (int i = threadIdx.x; i < CPW * COND_TOTAL; i += THREADS) {
                 const int c = i / COND_TOTAL, k = i - c * COND_TOTAL;
                 const int64_t gc = cand0 + c;
-                lds[L::CP + i] = gc < p.batch ? p.cproj[(size_t)(p.cproj_stride ? gc : 0) * COND_TOTAL + k] : 0.f;
+                lds[L::CP + c * CP_STRIDE + k] = gc < p.batch ? p.cproj[(size_t)(p.cproj_stride ? gc : 0) * COND_TOTAL + k] : 0.f;
             }
         }
         // x_T
@@ -362,13 +419,27 @@ struct MlpKernel {
         StepPlan sp = p.plan[0];
         fetch_noise(nz, p, sp, 0, cand0, wave, lane);
 
+#ifdef MPCD_PROF_LAYERS
+        // experiment build only: per-wave shader-clock cycles of each layer (work, then barrier wait)
+        uint64_t tacc[2 * 16] = {};
+        uint64_t tprev = __builtin_readcyclecounter();
+        auto bar = [&](int k) {
+            uint64_t t = __builtin_readcyclecounter();
+            tacc[2 * k] += t - tprev;
+            lds_barrier();
+            tprev = __builtin_readcyclecounter();
+            tacc[2 * k + 1] += tprev - t;
+        };
+#else
+        auto bar = [](int) { lds_barrier(); };
+#endif
         for (int s = 0; s < p.n_steps; ++s) {
             // Launder the weight base every step: the weights are loop-invariant, and without this
             // LICM hoists all 14 layers' loads out of the step loop (hundreds of live VGPRs -> spills).
             asm volatile("" : "+s"(wofs), "+v"(lane16));
             WFrag<A::K[1], A::N[1], mode_for<A::N[1]>()> w1;
             load_w(w1, W(1), wave, lane16);
-            lds_barrier();
+            bar(0);
             // this step's time projections -> LDS (first read by layer 1, after the next barrier)
             for (int i = threadIdx.x; i < COND_TOTAL / 4; i += THREADS)
                 reinterpret_cast<f32x4 *>(lds + L::TP)[i] =
@@ -379,73 +450,73 @@ struct MlpKernel {
             dump(p, lds + L::T1, L::ST1, 32, 0);
             WFrag<A::K[2], A::N[2], mode_for<A::N[2]>()> w2;
             load_w(w2, W(2), wave, lane16);
-            lds_barrier();
+            bar(1);
             hidden_layer<A::K[1], A::N[1], mode_for<A::N[1]>(), EPI_CMISH, NB>(w1, Bs(1), lds + L::T1, L::ST1, false, lds + L::S1, L::SS1, tp, cp,
                                                           0, has_ctx, wave, lane);
             dump(p, lds + L::S1, L::SS1, 32, 1);
             WFrag<A::K[3], A::N[3], mode_for<A::N[3]>()> w3;
             load_w(w3, W(3), wave, lane16);
-            lds_barrier();
+            bar(2);
             hidden_layer<A::K[2], A::N[2], mode_for<A::N[2]>(), EPI_MISH, NB>(w2, Bs(2), lds + L::S1, L::SS1, false, lds + L::T1, L::ST1, tp, cp,
                                                          0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 64, 2);
             WFrag<A::K[4], A::N[4], mode_for<A::N[4]>()> w4;
             load_w(w4, W(4), wave, lane16);
-            lds_barrier();
+            bar(3);
             hidden_layer<A::K[3], A::N[3], mode_for<A::N[3]>(), EPI_CMISH, NB>(w3, Bs(3), lds + L::T1, L::ST1, false, lds + L::C1 + 64, L::SC1,
                                                           tp, cp, 1, has_ctx, wave, lane);
             dump(p, lds + L::C1 + 64, L::SC1, 64, 3);
             WFrag<A::K[5], A::N[5], mode_for<A::N[5]>()> w5;
             load_w(w5, W(5), wave, lane16);
-            lds_barrier();
+            bar(4);
             hidden_layer<A::K[4], A::N[4], mode_for<A::N[4]>(), EPI_MISH, NB>(w4, Bs(4), lds + L::C1 + 64, L::SC1, false, lds + L::T1, L::ST1,
                                                          tp, cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 128, 4);
             WFrag<A::K[6], A::N[6], mode_for<A::N[6]>()> w6;
             load_w(w6, W(6), wave, lane16);
-            lds_barrier();
+            bar(5);
             hidden_layer<A::K[5], A::N[5], mode_for<A::N[5]>(), EPI_CMISH, NB>(w5, Bs(5), lds + L::T1, L::ST1, false, lds + L::C0 + 128,
                                                           L::SC0, tp, cp, 2, has_ctx, wave, lane);
             dump(p, lds + L::C0 + 128, L::SC0, 128, 5);
             WFrag<A::K[7], A::N[7], mode_for<A::N[7]>()> w7;
             load_w(w7, W(7), wave, lane16);
-            lds_barrier();
+            bar(6);
             hidden_layer<A::K[6], A::N[6], mode_for<A::N[6]>(), EPI_MISH, NB>(w6, Bs(6), lds + L::C0 + 128, L::SC0, false, lds + L::T1, L::ST1,
                                                          tp, cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 128, 6);
             WFrag<A::K[8], A::N[8], mode_for<A::N[8]>()> w8;
             load_w(w8, W(8), wave, lane16);
-            lds_barrier();
+            bar(7);
             hidden_layer<A::K[7], A::N[7], mode_for<A::N[7]>(), EPI_CMISH, NB>(w7, Bs(7), lds + L::T1, L::ST1, false, lds + L::C0, L::SC0, tp,
                                                           cp, 3, has_ctx, wave, lane);
             dump(p, lds + L::C0, L::SC0, 128, 7);
             WFrag<A::K[9], A::N[9], mode_for<A::N[9]>()> w9;
             load_w(w9, W(9), wave, lane16);
-            lds_barrier();
+            bar(8);
             hidden_layer<A::K[8], A::N[8], mode_for<A::N[8]>(), EPI_MISH, NB>(w8, Bs(8), lds + L::C0, L::SC0, false, lds + L::T1, L::ST1, tp, cp,
                                                          0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 64, 8);
             WFrag<A::K[10], A::N[10], mode_for<A::N[10]>()> w10;
             load_w(w10, W(10), wave, lane16);
-            lds_barrier();
+            bar(9);
             hidden_layer<A::K[9], A::N[9], mode_for<A::N[9]>(), EPI_CMISH, NB>(w9, Bs(9), lds + L::T1, L::ST1, false, lds + L::C1, L::SC1, tp,
                                                           cp, 4, has_ctx, wave, lane);
             dump(p, lds + L::C1, L::SC1, 64, 9);
             WFrag<A::K[11], A::N[11], mode_for<A::N[11]>()> w11;
             load_w(w11, W(11), wave, lane16);
-            lds_barrier();
+            bar(10);
             hidden_layer<A::K[10], A::N[10], mode_for<A::N[10]>(), EPI_MISH, NB>(w10, Bs(10), lds + L::C1, L::SC1, false, lds + L::T1, L::ST1,
                                                            tp, cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 32, 10);
             WFrag<A::K[12], A::N[12], mode_for<A::N[12]>()> w12;
             load_w(w12, W(12), wave, lane16);
-            lds_barrier();
+            bar(11);
             hidden_layer<A::K[11], A::N[11], mode_for<A::N[11]>(), EPI_CMISH, NB>(w11, Bs(11), lds + L::T1, L::ST1, false, lds + L::S1, L::SS1,
                                                             tp, cp, 5, has_ctx, wave, lane);
             dump(p, lds + L::S1, L::SS1, 32, 11);
             WFrag<A::K[13], A::N[13], PAIRED> w13;
             load_w(w13, W(13), wave, lane16);
-            lds_barrier();
+            bar(12);
             hidden_layer<A::K[12], A::N[12], mode_for<A::N[12]>(), EPI_NONE, NB>(w12, Bs(12), lds + L::S1, L::SS1, false, lds + L::T1, L::ST1,
                                                            tp, cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 32, 12);
@@ -460,9 +531,17 @@ struct MlpKernel {
                 sp = p.plan[s + 1];
                 fetch_noise(nz, p, sp, s + 1, cand0, wave, lane);
             }
-            lds_barrier();
+            bar(13);
             final_and_update(w13, Bs(13), lds, p, cur, s, cand0, nzc, wave, lane);
         }
+#ifdef MPCD_PROF_LAYERS
+        {
+            const uint64_t t = __builtin_readcyclecounter();
+            tacc[2 * 15] += t - tprev;
+            if (p.dbg && blockIdx.x < 8 && lane == 0)
+                for (int i = 0; i < 32; ++i) p.dbg[(blockIdx.x * 4 + wave) * 32 + i] = (float)tacc[i];
+        }
+#endif
     }
 };
 

@@ -523,6 +523,7 @@ int mpcd_sample(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr)
     HIP_TRY(hipEventRecord(c->ev0, st));
     if (d.kind == MPCD_NET_MLP) {
         MlpSampleArgs m{};
+        m.dbg = c->dbg;  // read only by the MPCD_PROF_LAYERS experiment build
         m.wpack = c->wpack.as<float>();
         m.plan = c->plan.as<StepPlan>();
         m.tproj = c->tproj.as<float>();
@@ -646,6 +647,15 @@ int mpcd_last_sample_ms(mpcd_ctx *c, float *ms)
     if (!c->timed) return fail(MPCD_ESTATE, "no sample call recorded");
     HIP_TRY(hipEventSynchronize(c->ev1));
     HIP_TRY(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return MPCD_OK;
+}
+
+// Not in mpcd.h: debug / profiling dump target (layer activations in mpcd_eps, per-layer cycles in
+// the MPCD_PROF_LAYERS experiment build). Null disables.
+int mpcd_debug_set(mpcd_ctx *c, float *dbg)
+{
+    if (!c) return fail(MPCD_EINVAL, "null argument");
+    c->dbg = dbg;
     return MPCD_OK;
 }
 

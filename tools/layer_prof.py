@@ -1,0 +1,38 @@
+"""Per-layer shader-clock breakdown of the MLP sampler (experiment build -DMPCD_PROF_LAYERS).
+
+  python -m mpc_via_diffusion_model_amd.build prof MPCD_PROF_LAYERS      # here
+  MPCD_LIB=mpc_via_diffusion_model_amd/libmpcd_prof.so python tools/layer_prof.py   # GPU box
+Prints cycles per step (work / barrier wait) for each segment, averaged over 32 waves of 8 WGs."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec  # noqa: E402
+from mpc_via_diffusion_model_amd import _native  # noqa: E402
+from oracle import nets  # noqa: E402
+
+torch.manual_seed(0)
+net = nets.ConditionedMLPNet(state_dim=2, horizon=32, context_dim=4)
+plan = DiffusionMPC(NetSpec("mlp", state_dim=2, horizon=32, context_dim=4), net.state_dict(),
+                    variance_schedule="exponential", n_diffusion_steps=100)
+ctx = torch.rand(1, 4) * 2 - 1
+B = int(os.environ.get("B", 4096))
+plan.sample_trajectories(ctx, B, 32, seed=1)
+dbg = torch.zeros(14 * 32 * 256, device="cuda")
+L = _native.lib()
+L.mpcd_debug_set.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+L.mpcd_debug_set(plan._ctx, ctypes.c_void_p(dbg.data_ptr()))
+plan.sample_trajectories(ctx, B, 32, seed=1)
+torch.cuda.synchronize()
+print(f"kernel ms {plan.last_sample_ms():.3f}")
+t = dbg[: 32 * 32].cpu().numpy().reshape(32, 32) / 100.0
+names = ["final+w1"] + [f"L{l}" for l in range(13)] + ["-", "tail"]
+tot = t.sum(1).mean()
+print(f"cycles/step per wave: {tot:.0f}")
+for k in range(16):
+    w, b = t[:, 2 * k].mean(), t[:, 2 * k + 1].mean()
+    print(f"{names[k]:>9}: work {w:8.0f}  wait {b:8.0f}   (work max {t[:, 2 * k].max():8.0f})")
