@@ -422,7 +422,9 @@ struct MlpKernel {
 #ifdef MPCD_PROF_LAYERS
         // experiment build only: per-wave shader-clock cycles of each layer (work, then barrier wait)
         uint64_t tacc[2 * 16] = {};
+        const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
         uint64_t tprev = __builtin_readcyclecounter();
+        const uint64_t ct0 = tprev;
         auto bar = [&](int k) {
             uint64_t t = __builtin_readcyclecounter();
             tacc[2 * k] += t - tprev;
@@ -540,6 +542,14 @@ struct MlpKernel {
             tacc[2 * 15] += t - tprev;
             if (p.dbg && blockIdx.x < 8 && lane == 0)
                 for (int i = 0; i < 32; ++i) p.dbg[(blockIdx.x * 4 + wave) * 32 + i] = (float)tacc[i];
+            if (p.dbg && threadIdx.x == 0) {  // per-block loop start / end (memrealtime, low 32 bits)
+                p.dbg[4096 + blockIdx.x * 2] = __builtin_bit_cast(float, (uint32_t)rt0);
+                p.dbg[4096 + blockIdx.x * 2 + 1] = __builtin_bit_cast(float, (uint32_t)__builtin_amdgcn_s_memrealtime());
+            }
+            if (p.dbg && blockIdx.x < 8 && threadIdx.x == 0) {  // shader clock = d(memtime) / d(memrealtime) x 100 MHz
+                p.dbg[8 * 4 * 32 + blockIdx.x * 2] = (float)(t - ct0);
+                p.dbg[8 * 4 * 32 + blockIdx.x * 2 + 1] = (float)(__builtin_amdgcn_s_memrealtime() - rt0);
+            }
         }
 #endif
     }

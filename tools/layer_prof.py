@@ -29,6 +29,16 @@ L.mpcd_debug_set(plan._ctx, ctypes.c_void_p(dbg.data_ptr()))
 plan.sample_trajectories(ctx, B, 32, seed=1)
 torch.cuda.synchronize()
 print(f"kernel ms {plan.last_sample_ms():.3f}")
+ck = dbg[8 * 4 * 32: 8 * 4 * 32 + 16].cpu().numpy().reshape(8, 2)
+se = dbg[4096: 4096 + 2 * 1024].cpu().view(torch.int32).numpy().astype(np.int64).reshape(-1, 2)
+se = se[se[:, 1] != 0]
+nb = len(se)
+base = se[:, 0].min()
+st, en = (se[:, 0] - base) / 100.0, (se[:, 1] - base) / 100.0  # microseconds
+print(f"blocks {nb}: loop start us min/med/max {st.min():.1f}/{np.median(st):.1f}/{st.max():.1f}; "
+      f"end min/med/max {en.min():.1f}/{np.median(en):.1f}/{en.max():.1f}")
+print("slowest blocks (id, start, end):", [(int(i), round(float(st[i]), 1), round(float(en[i]), 1)) for i in np.argsort(-en)[:6]])
+print(f"shader clock {float(np.median(ck[:, 0] / ck[:, 1])) * 0.1:.3f} GHz (memtime / memrealtime, 8 blocks)")
 t = dbg[: 32 * 32].cpu().numpy().reshape(32, 32) / 100.0
 names = ["final+w1"] + [f"L{l}" for l in range(13)] + ["-", "tail"]
 tot = t.sum(1).mean()
