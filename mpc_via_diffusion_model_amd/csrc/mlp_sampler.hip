@@ -28,6 +28,10 @@ constexpr int NLAYER = 14;
 constexpr int COND_TOTAL = 448;  // 32+64+128+128+64+32
 constexpr int CP_STRIDE = COND_TOTAL + 4;  // LDS cproj row stride (448 = 0 mod 64 banks: 16-way conflict)
 enum { EPI_NONE = 0, EPI_MISH = 1, EPI_CMISH = 2 };
+// CFG-DDPM with caller-supplied noise: its own instantiation, so the in-kernel-Philox variant has no
+// global load in the step loop (a conditional noise load made the compiler drain vmcnt(0), i.e. wait
+// for the next step's weight prefetch, every step).
+constexpr int MODE_DDPM_XN = 16;
 enum { SPLIT = 0, PAIRED = 1 };
 
 template <int D0>
@@ -57,14 +61,15 @@ __host__ __device__ constexpr int cond_off(int j) { return j == 0 ? 0 : j == 1 ?
 template <int D0, int NB>
 struct Lds {
     static constexpr int CPW = ROWS / NB;          // candidates per workgroup
-    static constexpr int SX = D0 + 4, ST1 = 132, SS1 = 36, SC1 = 132, SC0 = 260;
+    static constexpr int SX = D0 + 4, ST1 = 132, SS1 = 68, SC1 = 132, SC0 = 260;  // all = 4 mod 64 (banks)
     static constexpr int XB = 0;
     static constexpr int T1 = XB + CPW * SX;
     static constexpr int S1 = T1 + ROWS * ST1;
     static constexpr int C1 = S1 + ROWS * SS1;
     static constexpr int C0 = C1 + ROWS * SC1;
     static constexpr int TP = C0 + ROWS * SC0;     // this step's tproj [448]
-    static constexpr int BI = TP + COND_TOTAL;     // all 14 biases
+    static constexpr int BIC = TP + COND_TOTAL;    // biases of the cond layers in tproj column order
+    static constexpr int BI = BIC + COND_TOTAL;    // all 14 biases
     static constexpr int CP = BI + Arch<D0>::btotal();  // per-candidate cproj [CPW][448]
     static constexpr int total(bool ctx) { return CP + (ctx ? CPW * CP_STRIDE : 0); }
 };
@@ -111,6 +116,26 @@ MPCD_DEV void load_w(WFrag<K, N, MODE> &f, const float *__restrict__ wp, int wav
     }
 }
 
+// The step plan is read through the constant address space: scalar loads (lgkmcnt), so using it
+// never waits on the vector-memory queue that holds the next layers' weight prefetches.
+MPCD_DEV StepPlan load_plan(const StepPlan *plan, int s)
+{
+    typedef const __attribute__((address_space(4))) StepPlan *cplan_t;
+    const cplan_t q = (cplan_t)(uintptr_t)plan + s;
+    StepPlan r;
+    r.t = q->t;
+    r.flags = q->flags;
+    r.a = q->a;
+    r.b = q->b;
+    r.c1 = q->c1;
+    r.c2 = q->c2;
+    r.std = q->std;
+    r.sqan = q->sqan;
+    r.cn = q->cn;
+    r.pad = 0.f;
+    return r;
+}
+
 // Two independent 16-k chains, issued alternately: a v_mfma_f32_16x16x4_f32 whose C operand is the
 // previous MFMA's result waits 40 cycles instead of issuing at the 32-cycle pipe rate.
 MPCD_DEV void mfma4x2(const f32x4 &wa, const f32x4 &aa, f32x4 &acca, const f32x4 &wb, const f32x4 &ab, f32x4 &accb)
@@ -134,32 +159,21 @@ MPCD_DEV f32x4 mfma4(const f32x4 &w, const f32x4 &a, f32x4 acc)
     return acc;
 }
 
-// Ask the scheduler for NM x {1 MFMA, NV VALU}: the previous group's epilogue rides in the MFMA
-// issue gaps (32 cycles per v_mfma_f32_16x16x4_f32, ~24 of them free for VALU).
-template <int NM, int NV>
-MPCD_DEV void interleave()
-{
-#pragma unroll
-    for (int i = 0; i < NM; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
-    }
-}
-
 // Hidden layer. SPLIT (N = 32): wave w -> column tile (w & 1), n-tiles (w >> 1) + 2j.
 // PAIRED (N >= 64): wave w -> n-tiles w + 4j for BOTH column tiles, so each weight register feeds
 // two MFMAs and a wave holds only a quarter of the layer's weights.
 // in_shared: both column tiles read rows 0..15 (layer 0 with CFG: both branches see the same x).
 //
-// Schedule: the wave's output tiles form G groups of two independent accumulation chains (two
-// column tiles of one n-tile when T = 2, else the even / odd k-blocks of one tile, summed at the
-// end), so the MFMA pipe never waits on a dependent chain; group g's MFMAs are issued together
-// with group g-1's epilogue (bias, cond, Mish, ds_write), leaving only the last group's epilogue
-// exposed before the barrier. Activations, bias and cond operands are read from LDS up front.
+// The accumulators start from `init` (LDS, per output feature): the layer bias, or for the cond
+// layers tproj + bias (the time part of cond_mlp and the Linear bias, pre-summed when the step's
+// tproj is staged), so the epilogue adds only the context part on the context rows. Every wave
+// issues two independent accumulation chains alternately (two column tiles of one n-tile when
+// T = 2, else the even / odd k-blocks of one tile, summed at the end): f32 MFMA and VALU share the
+// SIMD's issue on gfx950, so VALU ops per output element are what the epilogue minimises.
 template <int K, int N, int MODE, int EPI, int NB>
-MPCD_DEV void hidden_layer(const WFrag<K, N, MODE> &f, const float *__restrict__ bias, const float *in, int in_stride,
-                           bool in_shared, float *out, int out_stride, const float *tp, const float *cp, int cond_j,
-                           bool has_ctx, int wave, int lane)
+MPCD_DEV void hidden_layer(const WFrag<K, N, MODE> &f, const float *init, const float *in, int in_stride,
+                           bool in_shared, float *out, int out_stride, const float *cp, int cond_j, bool has_ctx,
+                           int wave, int lane)
 {
     constexpr int T = WFrag<K, N, MODE>::T, KB = K / 16, NT = N / 16;
     constexpr int NCT = MODE == SPLIT ? 1 : 2;
@@ -178,84 +192,72 @@ MPCD_DEV void hidden_layer(const WFrag<K, N, MODE> &f, const float *__restrict__
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) a[c][kb] = *reinterpret_cast<const f32x4 *>(arow + kb * 16);
     }
-    f32x4 b4[T], cv[T][NCT];
+    f32x4 i4[T];
 #pragma unroll
-    for (int j = 0; j < T; ++j) {
-        const int n = ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q;
-        b4[j] = *reinterpret_cast<const f32x4 *>(bias + n);
-        if (EPI != EPI_CMISH) continue;
-        const f32x4 tc = *reinterpret_cast<const f32x4 *>(tp + cond_off(cond_j) + n);
-#pragma unroll
-        for (int c = 0; c < NCT; ++c) {
-            // NB == 2: column tile = branch (0: context, 1: masked -> time part only); NB == 1: all unmasked.
-            // Branch-free select (the masked rows take tc exactly): a wave-uniform branch around this
-            // LDS load let the masked rows consume a stale .w register (seen on gfx950 / ROCm 7.2).
-            const int ct = MODE == SPLIT ? (wave & 1) : c;
-            cv[j][c] = tc;
-            if (has_ctx) {
-                const int cand = NB == 2 ? col : ct * 16 + col;
-                const f32x4 cpv = *reinterpret_cast<const f32x4 *>(cp + cand * CP_STRIDE + cond_off(cond_j) + n);
-                const f32x4 sum = tc + cpv;
-                const bool take = NB == 1 || ct == 0;
-                cv[j][c].x = take ? sum.x : tc.x;
-                cv[j][c].y = take ? sum.y : tc.y;
-                cv[j][c].z = take ? sum.z : tc.z;
-                cv[j][c].w = take ? sum.w : tc.w;
-            }
-        }
-    }
+    for (int j = 0; j < T; ++j) i4[j] = *reinterpret_cast<const f32x4 *>(init + ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q);
 
     f32x4 acc[G][2];
-    auto chain = [&](int g) {
-        acc[g][0] = acc[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#ifdef MPCD_DIAG_NOMFMA
+    // timing diagnostic only (wrong results): no MFMAs, activations folded in so loads stay live
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        acc[g][0] = i4[BYJ ? g : 0] + a[BYJ ? 0 : g][0];
+        acc[g][1] = a[BYJ ? 1 % NCT : g][KB - 1] + f.v[BYJ ? g : 0][KB - 1];
+    }
+    if (false)
+#endif
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
         if (BYJ) {
+            acc[g][0] = acc[g][1] = i4[g];
 #pragma unroll
             for (int kb = 0; kb < KB; ++kb) mfma4x2(f.v[g][kb], a[0][kb], acc[g][0], f.v[g][kb], a[1][kb], acc[g][1]);
         } else {
+            acc[g][0] = i4[0];
+            acc[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int kb = 0; kb < KB; kb += 2)
                 mfma4x2(f.v[0][kb], a[g][kb], acc[g][0], f.v[0][kb + 1], a[g][kb + 1], acc[g][1]);
         }
-    };
-    auto store = [&](int j, int c, f32x4 v) {
+    }
+#pragma unroll
+    for (int t = 0; t < T * NCT; ++t) {
+        const int j = t / NCT, c = t % NCT;
         const int ct = MODE == SPLIT ? (wave & 1) : c;
         const int n = ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q;
-        v = v + b4[j];
-        if (EPI == EPI_CMISH) v = v + cv[j][c];
+        f32x4 v = BYJ ? acc[j][c] : acc[c][0] + acc[c][1];
+        // context part of cond_mlp: NB == 2 only on the context branch (column tile 0; the masked
+        // tile takes the time part alone, already in the accumulator), NB == 1 on every row. SPLIT
+        // layers know their tile at run time: multiply-add by an exact 0/1 factor, no branch.
+        if (EPI == EPI_CMISH && has_ctx && (NB == 1 || MODE == SPLIT || c == 0)) {
+            const int cand = NB == 2 ? col : ct * 16 + col;
+            const f32x4 cpv = *reinterpret_cast<const f32x4 *>(cp + cand * CP_STRIDE + cond_off(cond_j) + n);
+            if (NB == 2 && MODE == SPLIT) {
+                const float on = ct == 0 ? 1.0f : 0.0f;
+                v.x = __builtin_fmaf(cpv.x, on, v.x);
+                v.y = __builtin_fmaf(cpv.y, on, v.y);
+                v.z = __builtin_fmaf(cpv.z, on, v.z);
+                v.w = __builtin_fmaf(cpv.w, on, v.w);
+            } else {
+                v = v + cpv;
+            }
+        }
+#ifndef MPCD_DIAG_NOMISH
         if (EPI != EPI_NONE) {
             v.x = mish(v.x);
             v.y = mish(v.y);
             v.z = mish(v.z);
             v.w = mish(v.w);
         }
+#endif
         *reinterpret_cast<f32x4 *>(out + (size_t)(ct * 16 + col) * out_stride + n) = v;
-    };
-    auto epi = [&](int g) {
-        if (BYJ) {
-#pragma unroll
-            for (int c = 0; c < NCT; ++c) store(g, c, acc[g][c]);
-        } else {
-            store(0, g, acc[g][0] + acc[g][1]);
-        }
-    };
-    // MFMAs per group and the epilogue's VALU per MFMA slot (~16 VALU per output element incl. Mish)
-    constexpr int NM = BYJ ? KB * 4 * NCT : KB * 4;
-    constexpr int EPI_VALU = (BYJ ? NCT : 1) * 4 * (EPI == EPI_NONE ? 2 : 16);
-    constexpr int NV = (EPI_VALU + NM - 1) / NM;
-    chain(0);
-#pragma unroll
-    for (int g = 1; g < G; ++g) {
-        __builtin_amdgcn_sched_barrier(0);
-        chain(g);
-        epi(g - 1);
-        __builtin_amdgcn_sched_barrier(0);
     }
-    epi(G - 1);
 }
 
 template <int D0, int SMODE, bool CTX>
 struct MlpKernel {
     static constexpr int NB = (SMODE == MODE_DDIM || SMODE == MODE_EPS1) ? 1 : 2;
+    static constexpr bool IS_DDPM = SMODE == MODE_DDPM_CFG || SMODE == MODE_DDPM_XN;
     using A = Arch<D0>;
     using L = Lds<D0, NB>;
     static constexpr int CPW = L::CPW;
@@ -270,7 +272,8 @@ struct MlpKernel {
         const int col = lane & 15, q = lane >> 4;
         f32x4 acc[T][2];
 #pragma unroll
-        for (int j = 0; j < T; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < T; ++j)  // accumulators start from the bias (idle tiles read unused LDS)
+            acc[j][0] = acc[j][1] = *reinterpret_cast<const f32x4 *>(bias + (wave + 4 * j) * 16 + 4 * q);
         const float *arow0 = lds + L::T1 + (size_t)col * L::ST1 + 4 * q;
         const float *arow1 = arow0 + 16 * L::ST1;
 #pragma unroll
@@ -287,7 +290,6 @@ struct MlpKernel {
             const int nt = wave + 4 * j;
             if (NT % 4 != 0 && nt >= NT) continue;
             const int n = nt * 16 + 4 * q;
-            const f32x4 b4 = *reinterpret_cast<const f32x4 *>(bias + n);
 #pragma unroll
             for (int g = 0; g < (NB == 2 ? 1 : 2); ++g) {
                 // NB == 2: one candidate per lane column, eps_c = tile 0, eps_u = tile 1
@@ -295,8 +297,8 @@ struct MlpKernel {
                 const int cl = NB == 2 ? col : g * 16 + col;
                 float *xp = lds + L::XB + (size_t)cl * L::SX + n;
                 const f32x4 x = *reinterpret_cast<const f32x4 *>(xp);
-                const f32x4 ec = acc[j][NB == 2 ? 0 : g] + b4;
-                const f32x4 eu = acc[j][1] + b4;
+                const f32x4 ec = acc[j][NB == 2 ? 0 : g];
+                const f32x4 eu = acc[j][1];
                 if (SMODE == MODE_EPS || SMODE == MODE_EPS1) {
                     const int64_t gc = cand0 + cl;
                     if (gc < p.batch) {
@@ -310,7 +312,7 @@ struct MlpKernel {
                 for (int r = 0; r < 4; ++r) {
                     const float xv = x[r];
                     float o;
-                    if (SMODE == MODE_DDPM_CFG) {
+                    if (IS_DDPM) {
                         const float x0c = sp.a * xv - sp.b * ec[r];
                         const float x0u = sp.a * xv - sp.b * eu[r];
                         float x0 = p.wp1 * x0c - p.wf * x0u;
@@ -349,7 +351,7 @@ struct MlpKernel {
         for (int j = 0; j < T; ++j)
 #pragma unroll
             for (int g = 0; g < NB; ++g) nz[j][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (SMODE != MODE_DDPM_CFG || !(sp.flags & PLAN_NOISE)) return;  // DDIM: sigma = 0
+        if (!IS_DDPM || !(sp.flags & PLAN_NOISE)) return;  // DDIM: sigma = 0
         const int col = lane & 15, q = lane >> 4;
 #pragma unroll
         for (int j = 0; j < T; ++j) {
@@ -358,7 +360,7 @@ struct MlpKernel {
             const int n = nt * 16 + 4 * q;
             const int64_t gc = cand0 + col;  // DDPM-CFG only: NB == 2, one candidate per column
             if (gc >= p.batch) continue;
-            if (p.noise)
+            if (SMODE == MODE_DDPM_XN)
                 nz[j][0] = *reinterpret_cast<const f32x4 *>(p.noise + ((size_t)(s + 1) * p.batch + gc) * D0 + n);
             else
                 nz[j][0] = philox_normal4(p.seed, (uint64_t)(p.global_offset + gc), (uint32_t)(s + 1), (uint32_t)(n >> 2));
@@ -391,6 +393,10 @@ struct MlpKernel {
         // biases of every layer -> LDS (read in each epilogue instead of a global round trip)
         for (int l = 0; l < NLAYER; ++l)
             for (int i = threadIdx.x; i < A::N[l]; i += THREADS) lds[L::BI + A::boff(l) + i] = wp[A::woff(l) + A::K[l] * A::N[l] + i];
+        // biases of the cond layers (1, 3, ..., 11) laid out like tproj: TP = tproj[s] + BIC per step
+        for (int j = 0; j < 6; ++j)
+            for (int i = threadIdx.x; i < A::N[2 * j + 1]; i += THREADS)
+                lds[L::BIC + cond_off(j) + i] = wp[A::woff(2 * j + 1) + A::K[2 * j + 1] * A::N[2 * j + 1] + i];
         // per-candidate context projections (constant over the denoise loop)
         if (has_ctx) {
             for (int i = threadIdx.x; i < CPW * COND_TOTAL; i += THREADS) {
@@ -416,8 +422,11 @@ struct MlpKernel {
         load_w(w0, W(0), wave, lane16);
         constexpr int NZT = WFrag<32, D0, PAIRED>::T;
         f32x4 nz[NZT][NB];
-        StepPlan sp = p.plan[0];
+        StepPlan sp = load_plan(p.plan, 0);
         fetch_noise(nz, p, sp, 0, cand0, wave, lane);
+        // tproj of step s, prefetched one step ahead (threads >= COND_TOTAL/4 load a duplicate, unused)
+        const int tpi = threadIdx.x < COND_TOTAL / 4 ? (int)threadIdx.x : 0;
+        f32x4 tpre = reinterpret_cast<const f32x4 *>(p.tproj)[tpi];
 
 #ifdef MPCD_PROF_LAYERS
         // experiment build only: per-wave shader-clock cycles of each layer (work, then barrier wait)
@@ -442,87 +451,75 @@ struct MlpKernel {
             WFrag<A::K[1], A::N[1], mode_for<A::N[1]>()> w1;
             load_w(w1, W(1), wave, lane16);
             bar(0);
-            // this step's time projections -> LDS (first read by layer 1, after the next barrier)
-            for (int i = threadIdx.x; i < COND_TOTAL / 4; i += THREADS)
-                reinterpret_cast<f32x4 *>(lds + L::TP)[i] =
-                    reinterpret_cast<const f32x4 *>(p.tproj + (size_t)s * COND_TOTAL)[i];
+            // this step's time projections + cond-layer biases -> LDS (first read by layer 1, after
+            // the next barrier); fetch the next step's
+            static_assert(COND_TOTAL / 4 <= THREADS, "tproj staging");
+            if (threadIdx.x < COND_TOTAL / 4)
+                reinterpret_cast<f32x4 *>(lds + L::TP)[tpi] = tpre + reinterpret_cast<const f32x4 *>(lds + L::BIC)[tpi];
+            tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 1 < p.n_steps ? s + 1 : s) * COND_TOTAL)[tpi];
             const float *tp = lds + L::TP, *cp = lds + L::CP;
-            hidden_layer<A::K[0], A::N[0], mode_for<A::N[0]>(), EPI_MISH, NB>(w0, Bs(0), lds + L::XB, L::SX, NB == 2, lds + L::T1, L::ST1, tp,
-                                                         cp, 0, has_ctx, wave, lane);
+            hidden_layer<A::K[0], A::N[0], mode_for<A::N[0]>(), EPI_MISH, NB>(w0, Bs(0), lds + L::XB, L::SX, NB == 2, lds + L::T1, L::ST1, cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 32, 0);
             WFrag<A::K[2], A::N[2], mode_for<A::N[2]>()> w2;
             load_w(w2, W(2), wave, lane16);
             bar(1);
-            hidden_layer<A::K[1], A::N[1], mode_for<A::N[1]>(), EPI_CMISH, NB>(w1, Bs(1), lds + L::T1, L::ST1, false, lds + L::S1, L::SS1, tp, cp,
-                                                          0, has_ctx, wave, lane);
+            hidden_layer<A::K[1], A::N[1], mode_for<A::N[1]>(), EPI_CMISH, NB>(w1, tp + cond_off(0), lds + L::T1, L::ST1, false, lds + L::S1, L::SS1, cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::S1, L::SS1, 32, 1);
             WFrag<A::K[3], A::N[3], mode_for<A::N[3]>()> w3;
             load_w(w3, W(3), wave, lane16);
             bar(2);
-            hidden_layer<A::K[2], A::N[2], mode_for<A::N[2]>(), EPI_MISH, NB>(w2, Bs(2), lds + L::S1, L::SS1, false, lds + L::T1, L::ST1, tp, cp,
-                                                         0, has_ctx, wave, lane);
+            hidden_layer<A::K[2], A::N[2], mode_for<A::N[2]>(), EPI_MISH, NB>(w2, Bs(2), lds + L::S1, L::SS1, false, lds + L::T1, L::ST1, cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 64, 2);
             WFrag<A::K[4], A::N[4], mode_for<A::N[4]>()> w4;
             load_w(w4, W(4), wave, lane16);
             bar(3);
-            hidden_layer<A::K[3], A::N[3], mode_for<A::N[3]>(), EPI_CMISH, NB>(w3, Bs(3), lds + L::T1, L::ST1, false, lds + L::C1 + 64, L::SC1,
-                                                          tp, cp, 1, has_ctx, wave, lane);
+            hidden_layer<A::K[3], A::N[3], mode_for<A::N[3]>(), EPI_CMISH, NB>(w3, tp + cond_off(1), lds + L::T1, L::ST1, false, lds + L::C1 + 64, L::SC1, cp, 1, has_ctx, wave, lane);
             dump(p, lds + L::C1 + 64, L::SC1, 64, 3);
             WFrag<A::K[5], A::N[5], mode_for<A::N[5]>()> w5;
             load_w(w5, W(5), wave, lane16);
             bar(4);
-            hidden_layer<A::K[4], A::N[4], mode_for<A::N[4]>(), EPI_MISH, NB>(w4, Bs(4), lds + L::C1 + 64, L::SC1, false, lds + L::T1, L::ST1,
-                                                         tp, cp, 0, has_ctx, wave, lane);
+            hidden_layer<A::K[4], A::N[4], mode_for<A::N[4]>(), EPI_MISH, NB>(w4, Bs(4), lds + L::C1 + 64, L::SC1, false, lds + L::T1, L::ST1, cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 128, 4);
             WFrag<A::K[6], A::N[6], mode_for<A::N[6]>()> w6;
             load_w(w6, W(6), wave, lane16);
             bar(5);
-            hidden_layer<A::K[5], A::N[5], mode_for<A::N[5]>(), EPI_CMISH, NB>(w5, Bs(5), lds + L::T1, L::ST1, false, lds + L::C0 + 128,
-                                                          L::SC0, tp, cp, 2, has_ctx, wave, lane);
+            hidden_layer<A::K[5], A::N[5], mode_for<A::N[5]>(), EPI_CMISH, NB>(w5, tp + cond_off(2), lds + L::T1, L::ST1, false, lds + L::C0 + 128, L::SC0, cp, 2, has_ctx, wave, lane);
             dump(p, lds + L::C0 + 128, L::SC0, 128, 5);
             WFrag<A::K[7], A::N[7], mode_for<A::N[7]>()> w7;
             load_w(w7, W(7), wave, lane16);
             bar(6);
-            hidden_layer<A::K[6], A::N[6], mode_for<A::N[6]>(), EPI_MISH, NB>(w6, Bs(6), lds + L::C0 + 128, L::SC0, false, lds + L::T1, L::ST1,
-                                                         tp, cp, 0, has_ctx, wave, lane);
+            hidden_layer<A::K[6], A::N[6], mode_for<A::N[6]>(), EPI_MISH, NB>(w6, Bs(6), lds + L::C0 + 128, L::SC0, false, lds + L::T1, L::ST1, cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 128, 6);
             WFrag<A::K[8], A::N[8], mode_for<A::N[8]>()> w8;
             load_w(w8, W(8), wave, lane16);
             bar(7);
-            hidden_layer<A::K[7], A::N[7], mode_for<A::N[7]>(), EPI_CMISH, NB>(w7, Bs(7), lds + L::T1, L::ST1, false, lds + L::C0, L::SC0, tp,
-                                                          cp, 3, has_ctx, wave, lane);
+            hidden_layer<A::K[7], A::N[7], mode_for<A::N[7]>(), EPI_CMISH, NB>(w7, tp + cond_off(3), lds + L::T1, L::ST1, false, lds + L::C0, L::SC0, cp, 3, has_ctx, wave, lane);
             dump(p, lds + L::C0, L::SC0, 128, 7);
             WFrag<A::K[9], A::N[9], mode_for<A::N[9]>()> w9;
             load_w(w9, W(9), wave, lane16);
             bar(8);
-            hidden_layer<A::K[8], A::N[8], mode_for<A::N[8]>(), EPI_MISH, NB>(w8, Bs(8), lds + L::C0, L::SC0, false, lds + L::T1, L::ST1, tp, cp,
-                                                         0, has_ctx, wave, lane);
+            hidden_layer<A::K[8], A::N[8], mode_for<A::N[8]>(), EPI_MISH, NB>(w8, Bs(8), lds + L::C0, L::SC0, false, lds + L::T1, L::ST1, cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 64, 8);
             WFrag<A::K[10], A::N[10], mode_for<A::N[10]>()> w10;
             load_w(w10, W(10), wave, lane16);
             bar(9);
-            hidden_layer<A::K[9], A::N[9], mode_for<A::N[9]>(), EPI_CMISH, NB>(w9, Bs(9), lds + L::T1, L::ST1, false, lds + L::C1, L::SC1, tp,
-                                                          cp, 4, has_ctx, wave, lane);
+            hidden_layer<A::K[9], A::N[9], mode_for<A::N[9]>(), EPI_CMISH, NB>(w9, tp + cond_off(4), lds + L::T1, L::ST1, false, lds + L::C1, L::SC1, cp, 4, has_ctx, wave, lane);
             dump(p, lds + L::C1, L::SC1, 64, 9);
             WFrag<A::K[11], A::N[11], mode_for<A::N[11]>()> w11;
             load_w(w11, W(11), wave, lane16);
             bar(10);
-            hidden_layer<A::K[10], A::N[10], mode_for<A::N[10]>(), EPI_MISH, NB>(w10, Bs(10), lds + L::C1, L::SC1, false, lds + L::T1, L::ST1,
-                                                           tp, cp, 0, has_ctx, wave, lane);
+            hidden_layer<A::K[10], A::N[10], mode_for<A::N[10]>(), EPI_MISH, NB>(w10, Bs(10), lds + L::C1, L::SC1, false, lds + L::T1, L::ST1, cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 32, 10);
             WFrag<A::K[12], A::N[12], mode_for<A::N[12]>()> w12;
             load_w(w12, W(12), wave, lane16);
             bar(11);
-            hidden_layer<A::K[11], A::N[11], mode_for<A::N[11]>(), EPI_CMISH, NB>(w11, Bs(11), lds + L::T1, L::ST1, false, lds + L::S1, L::SS1,
-                                                            tp, cp, 5, has_ctx, wave, lane);
+            hidden_layer<A::K[11], A::N[11], mode_for<A::N[11]>(), EPI_CMISH, NB>(w11, tp + cond_off(5), lds + L::T1, L::ST1, false, lds + L::S1, L::SS1, cp, 5, has_ctx, wave, lane);
             dump(p, lds + L::S1, L::SS1, 32, 11);
             WFrag<A::K[13], A::N[13], PAIRED> w13;
             load_w(w13, W(13), wave, lane16);
             bar(12);
-            hidden_layer<A::K[12], A::N[12], mode_for<A::N[12]>(), EPI_NONE, NB>(w12, Bs(12), lds + L::S1, L::SS1, false, lds + L::T1, L::ST1,
-                                                           tp, cp, 0, has_ctx, wave, lane);
+            hidden_layer<A::K[12], A::N[12], mode_for<A::N[12]>(), EPI_NONE, NB>(w12, Bs(12), lds + L::S1, L::SS1, false, lds + L::T1, L::ST1, cp, 0, has_ctx, wave, lane);
             dump(p, lds + L::T1, L::ST1, 32, 12);
-            if (s + 1 < p.n_steps) load_w(w0, W(0), wave, lane16);
             const StepPlan cur = sp;
             f32x4 nzc[NZT][NB];
 #pragma unroll
@@ -530,9 +527,12 @@ struct MlpKernel {
 #pragma unroll
                 for (int g = 0; g < NB; ++g) nzc[j][g] = nz[j][g];
             if (s + 1 < p.n_steps) {
-                sp = p.plan[s + 1];
+                sp = load_plan(p.plan, s + 1);
                 fetch_noise(nz, p, sp, s + 1, cand0, wave, lane);
             }
+            // next step's layer-0 weights; unconditional: a path-dependent load count makes the
+            // compiler drain vmcnt(0) at the next use
+            load_w(w0, W(0), wave, lane16);
             bar(13);
             final_and_update(w13, Bs(13), lds, p, cur, s, cand0, nzc, wave, lane);
         }
@@ -565,6 +565,7 @@ template <int D0, int SMODE, bool CTX>
 hipError_t launch_impl(const MlpSampleArgs &a, hipStream_t stream)
 {
     using L = Lds<D0, MlpKernel<D0, SMODE, CTX>::NB>;
+    static_assert(sizeof(float) * L::total(CTX) <= 160 * 1024, "LDS budget (160 KiB per CU)");
     const size_t lds_bytes = sizeof(float) * L::total(CTX);
     static bool attr_set = false;
     if (!attr_set) {
@@ -583,7 +584,9 @@ hipError_t launch_d0(const MlpSampleArgs &a, hipStream_t stream)
 {
     const bool ctx = a.cproj != nullptr;
     switch (a.mode) {
-    case MODE_DDPM_CFG: return ctx ? launch_impl<D0, MODE_DDPM_CFG, true>(a, stream) : launch_impl<D0, MODE_DDPM_CFG, false>(a, stream);
+    case MODE_DDPM_CFG:
+        if (a.noise) return ctx ? launch_impl<D0, MODE_DDPM_XN, true>(a, stream) : launch_impl<D0, MODE_DDPM_XN, false>(a, stream);
+        return ctx ? launch_impl<D0, MODE_DDPM_CFG, true>(a, stream) : launch_impl<D0, MODE_DDPM_CFG, false>(a, stream);
     case MODE_DDIM_CFG: return ctx ? launch_impl<D0, MODE_DDIM_CFG, true>(a, stream) : launch_impl<D0, MODE_DDIM_CFG, false>(a, stream);
     case MODE_DDIM: return ctx ? launch_impl<D0, MODE_DDIM, true>(a, stream) : launch_impl<D0, MODE_DDIM, false>(a, stream);
     case MODE_EPS: return ctx ? launch_impl<D0, MODE_EPS, true>(a, stream) : launch_impl<D0, MODE_EPS, false>(a, stream);
