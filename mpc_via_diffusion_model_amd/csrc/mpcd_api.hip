@@ -215,6 +215,10 @@ struct mpcd_ctx {
     // workspace
     DevBuf plan, tproj, cproj, flag, unet_ws;
     std::vector<StepPlan> plan_host;
+    // plan + tproj on the device are reused while the plan, net and schedule are unchanged (the
+    // time projections do not depend on the context, so a control loop computes them once)
+    std::vector<StepPlan> plan_cached;
+    bool plan_cached_valid = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     float *dbg = nullptr;  // debug dump target for mpcd_eps (mpcd_debug_set)
@@ -456,6 +460,7 @@ int mpcd_load_net(mpcd_ctx *c, const mpcd_net_desc *desc, const float *blob, siz
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
     c->net_loaded = false;
+    c->plan_cached_valid = false;
     return upload_net(c, *desc, blob, n_floats);
 }
 
@@ -467,6 +472,7 @@ int mpcd_set_schedule(mpcd_ctx *c, const float *tables, int32_t n_steps, const f
     for (int t = 0; t < n_steps; ++t)
         c->post_std[t] = post_std ? post_std[t] : sqrtf(expf(tables[(size_t)T_PLVC * n_steps + t]));
     c->n_steps = n_steps;
+    c->plan_cached_valid = false;
     return MPCD_OK;
 }
 
@@ -498,16 +504,22 @@ int mpcd_sample(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr)
     int rc = build_plan(c, a, c->plan_host);
     if (rc) return rc;
     const int S = (int)c->plan_host.size();
-    if ((rc = c->plan.ensure(sizeof(StepPlan) * S))) return rc;
-    HIP_TRY(hipMemcpyAsync(c->plan.p, c->plan_host.data(), sizeof(StepPlan) * S, hipMemcpyHostToDevice, st));
-    if ((rc = c->tproj.ensure(sizeof(float) * (size_t)S * c->cond_total))) return rc;
     const CondLayer *cl = c->cond_layers.as<CondLayer>();
-    const float *P = c->params.as<float>();
-    // time MLP = the first four tensors of the blob
-    const float *tw1 = P, *tb1 = tw1 + 128 * 32, *tw2 = tb1 + 128, *tb2 = tw2 + 32 * 128;
-    launch_time_prologue(c->plan.as<StepPlan>(), S, tw1, tb1, tw2, tb2, cl, c->n_cond, c->cond_dim, c->cond_total,
-                         c->tproj.as<float>(), st);
-    HIP_TRY(hipGetLastError());
+    const bool reuse = c->plan_cached_valid && c->plan_cached.size() == c->plan_host.size() &&
+                       memcmp(c->plan_cached.data(), c->plan_host.data(), sizeof(StepPlan) * S) == 0;
+    if (!reuse) {
+        if ((rc = c->plan.ensure(sizeof(StepPlan) * S))) return rc;
+        HIP_TRY(hipMemcpyAsync(c->plan.p, c->plan_host.data(), sizeof(StepPlan) * S, hipMemcpyHostToDevice, st));
+        if ((rc = c->tproj.ensure(sizeof(float) * (size_t)S * c->cond_total))) return rc;
+        const float *P = c->params.as<float>();
+        // time MLP = the first four tensors of the blob
+        const float *tw1 = P, *tb1 = tw1 + 128 * 32, *tw2 = tb1 + 128, *tb2 = tw2 + 32 * 128;
+        launch_time_prologue(c->plan.as<StepPlan>(), S, tw1, tb1, tw2, tb2, cl, c->n_cond, c->cond_dim, c->cond_total,
+                             c->tproj.as<float>(), st);
+        HIP_TRY(hipGetLastError());
+        c->plan_cached = c->plan_host;
+        c->plan_cached_valid = true;
+    }
     const float *cproj = nullptr;
     int64_t cstride = 0;
     if (d.context_dim > 0) {
@@ -587,6 +599,7 @@ int mpcd_eps(mpcd_ctx *c, const float *x, int32_t t, const float *context, int32
     StepPlan sp{};
     sp.t = t;
     c->plan_host.assign(1, sp);
+    c->plan_cached_valid = false;  // plan and tproj are overwritten below
     int rc;
     if ((rc = c->plan.ensure(sizeof(StepPlan)))) return rc;
     HIP_TRY(hipMemcpyAsync(c->plan.p, c->plan_host.data(), sizeof(StepPlan), hipMemcpyHostToDevice, st));

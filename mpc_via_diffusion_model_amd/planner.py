@@ -299,15 +299,17 @@ class DiffusionMPC:
         ctx = torch.from_numpy(self.normalize_condition(x0)[None])
         u_norm = self.sample_trajectories(ctx, n_samples, self.spec.horizon, w, sample_fn, n_wo_noise, ddim_steps,
                                           clamp_x0, seed, offset, noise)
-        flag = None
+        # LimitsNormalizer's clip flag is global over the whole batch: one rank's own flag, the OR
+        # over ranks, or provably zero (DDPM whose last posterior mean stays in range) -> no exchange
         sampler = self._sampler_id(sample_fn)
-        if size > 1 and not (sampler == N.MPCD_DDPM_CFG and self.ddpm_final_in_range):
+        if size == 1:
+            flag = self.clip_flag(u_norm)
+        elif sampler == N.MPCD_DDPM_CFG and self.ddpm_final_in_range:
+            flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+        else:
             flag = D.any_flag(self.clip_flag(u_norm), group)
         cost_local = self.rollout_cost(system, x0, u_norm, flag)
         idx, best, row, costs = D.select(cost_local, u_norm, self.argmin, group)
-        if flag is None:
-            # single rank: the flag of the whole batch; provably-zero case on several ranks
-            flag = self.clip_flag(u_norm) if size == 1 else torch.zeros(1, dtype=torch.int32, device=self.device)
         u_best = self.unnormalize_states(row[None], flag)[0]
         u_host = u_best.cpu().numpy()
         return MPCResult(u0=u_host[0].copy(), u_best=u_host, best_cost=best, best_index=idx, costs=costs,
