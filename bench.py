@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--dtype", default="f32x3", choices=["f32", "f32x3"],
+                    help="MLP GEMM numerics: exact fp32 MFMA, or fp32-accurate split-bf16 MFMA")
     args = ap.parse_args()
 
     rank, world, local = _rank_env()
@@ -85,7 +87,7 @@ def main():
 
     torch.manual_seed(0)
     net = nets.ConditionedMLPNet(state_dim=CFG["d"], horizon=CFG["H"], context_dim=CFG["C"])
-    spec = NetSpec("mlp", state_dim=CFG["d"], horizon=CFG["H"], context_dim=CFG["C"])
+    spec = NetSpec("mlp", state_dim=CFG["d"], horizon=CFG["H"], context_dim=CFG["C"], dtype=args.dtype)
     plan = DiffusionMPC(spec, net.state_dict(), variance_schedule=CFG["schedule"], n_diffusion_steps=CFG["N"])
     del net
     system = systems.get(CFG["system"])

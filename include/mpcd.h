@@ -42,7 +42,14 @@ enum mpcd_net_kind {
     MPCD_NET_UNET = 2,  /* ConditionedTemporalUnet (temporal_unet.py:189-358) or TemporalUnet (:28-187) */
 };
 
-enum mpcd_dtype { MPCD_F32 = 0, MPCD_F16 = 1 };
+/* GEMM numerics of the noise-net.
+ * MPCD_F32:   exact fp32 MFMA (v_mfma_f32_16x16x4_f32: one rounding per product, an fmaf chain).
+ * MPCD_F16:   fp16 hidden activations (SURVEY cfg 5) - not built, MPCD_EUNSUP.
+ * MPCD_F32X3: fp32-accurate split-bf16 MFMA (MLP only): each fp32 operand = three bf16 terms, the six
+ *             partial products >= 2^-16 of the leading one accumulated in fp32 (error at the level of
+ *             the fp32 MFMA's). Needs a context shared by all candidates (or none); a per-candidate
+ *             context runs the MPCD_F32 kernel. */
+enum mpcd_dtype { MPCD_F32 = 0, MPCD_F16 = 1, MPCD_F32X3 = 2 };
 
 typedef struct {
     int32_t kind;          /* mpcd_net_kind */

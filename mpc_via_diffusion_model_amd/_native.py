@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MPCD_LIB") or os.path.join(_HERE, "libmpcd.so")
 
 MPCD_NET_MLP, MPCD_NET_UNET = 1, 2
-MPCD_F32, MPCD_F16 = 0, 1
+MPCD_F32, MPCD_F16, MPCD_F32X3 = 0, 1, 2
 MPCD_DDPM_CFG, MPCD_DDIM_CFG, MPCD_DDIM = 0, 1, 2
 MPCD_COST_CANONICAL, MPCD_COST_CALMPC = 0, 1
 

@@ -19,42 +19,15 @@
 #include <hip/hip_runtime.h>
 
 #include "internal.h"
+#include "mlp_common.h"
 
 namespace {
+using namespace mlpc;
 
 constexpr int ROWS = 32;
 constexpr int THREADS = 256;
-constexpr int NLAYER = 14;
-constexpr int COND_TOTAL = 448;  // 32+64+128+128+64+32
 constexpr int CP_STRIDE = COND_TOTAL + 4;  // LDS cproj row stride (448 = 0 mod 64 banks: 16-way conflict)
-enum { EPI_NONE = 0, EPI_MISH = 1, EPI_CMISH = 2 };
-// CFG-DDPM with caller-supplied noise: its own instantiation, so the in-kernel-Philox variant has no
-// global load in the step loop (a conditional noise load made the compiler drain vmcnt(0), i.e. wait
-// for the next step's weight prefetch, every step).
-constexpr int MODE_DDPM_XN = 16;
 enum { SPLIT = 0, PAIRED = 1 };
-
-template <int D0>
-struct Arch {
-    static constexpr int K[NLAYER] = {D0, 32, 32, 64, 64, 128, 128, 128, 256, 64, 128, 32, 32, 32};
-    static constexpr int N[NLAYER] = {32, 32, 64, 64, 128, 128, 128, 128, 64, 64, 32, 32, 32, D0};
-    // Loop form (not recursion) so the device inliner folds every call to a constant.
-    __host__ __device__ static constexpr int woff(int l) {
-        int o = 0;
-        for (int i = 0; i < l; ++i) o += K[i] * N[i] + N[i];
-        return o;
-    }
-    static constexpr int total() { return woff(NLAYER); }
-    __host__ __device__ static constexpr int boff(int l) {  // biases staged in LDS
-        int o = 0;
-        for (int i = 0; i < l; ++i) o += N[i];
-        return o;
-    }
-    static constexpr int btotal() { return boff(NLAYER); }
-};
-
-// cond block j (0..5) -> column offset in the 448-wide tables
-__host__ __device__ constexpr int cond_off(int j) { return j == 0 ? 0 : j == 1 ? 32 : j == 2 ? 96 : j == 3 ? 224 : j == 4 ? 352 : 416; }
 
 // ---- LDS layout (floats). Row strides are width + 4 so the 16 rows a ds_read_b128 lane group
 // touches land on different 16-byte bank slots.
@@ -114,26 +87,6 @@ MPCD_DEV void load_w(WFrag<K, N, MODE> &f, const float *__restrict__ wp, int wav
             f.v[j][kb] = __builtin_bit_cast(f32x4, r);
         }
     }
-}
-
-// The step plan is read through the constant address space: scalar loads (lgkmcnt), so using it
-// never waits on the vector-memory queue that holds the next layers' weight prefetches.
-MPCD_DEV StepPlan load_plan(const StepPlan *plan, int s)
-{
-    typedef const __attribute__((address_space(4))) StepPlan *cplan_t;
-    const cplan_t q = (cplan_t)(uintptr_t)plan + s;
-    StepPlan r;
-    r.t = q->t;
-    r.flags = q->flags;
-    r.a = q->a;
-    r.b = q->b;
-    r.c1 = q->c1;
-    r.c2 = q->c2;
-    r.std = q->std;
-    r.sqan = q->sqan;
-    r.cn = q->cn;
-    r.pad = 0.f;
-    return r;
 }
 
 // Two independent 16-k chains, issued alternately: a v_mfma_f32_16x16x4_f32 whose C operand is the
@@ -272,8 +225,10 @@ struct MlpKernel {
         const int col = lane & 15, q = lane >> 4;
         f32x4 acc[T][2];
 #pragma unroll
-        for (int j = 0; j < T; ++j)  // accumulators start from the bias (idle tiles read unused LDS)
-            acc[j][0] = acc[j][1] = *reinterpret_cast<const f32x4 *>(bias + (wave + 4 * j) * 16 + 4 * q);
+        for (int j = 0; j < T; ++j) {  // accumulators start from the bias (idle tiles read n-tile 0, unused)
+            const int nt = (NT % 4 == 0 || wave + 4 * j < NT) ? wave + 4 * j : 0;
+            acc[j][0] = acc[j][1] = *reinterpret_cast<const f32x4 *>(bias + nt * 16 + 4 * q);
+        }
         const float *arow0 = lds + L::T1 + (size_t)col * L::ST1 + 4 * q;
         const float *arow1 = arow0 + 16 * L::ST1;
 #pragma unroll

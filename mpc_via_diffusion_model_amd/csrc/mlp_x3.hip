@@ -1,0 +1,585 @@
+// Persistent CFG-DDPM / DDIM sampler for the MLP noise-net, fp32-accurate split-bf16 GEMMs.
+//
+// Same schedule as mlp_sampler.hip (one launch = every denoise step for every candidate; a
+// 256-thread workgroup owns 32 rows = 16 candidates x {context, masked} for CFG or 32 candidates
+// for the 3-arg net; activations and x stay in LDS; weights stream from L2 one layer ahead), but the
+// 14 Linear layers run on v_mfma_f32_16x16x32_bf16 instead of the f32 MFMA.
+//
+// Why: on gfx950 the f32 MFMA runs at the f32 VALU rate and occupies the SIMD's vector issue for
+// its whole 32 cycles, so the exact-f32 kernel is bound by MFMA + VALU issue.
+// bf16 MFMA is 16x faster per MAC. Numerics stay fp32: every fp32 operand is split into three bf16
+// terms, x = x0 + x1 + x2 (each level round-to-nearest on the remainder of the previous one, so the
+// three carry x's 24-bit significand to ~2^-27), and every dot product accumulates the six partial
+// products whose weight is at least 2^-16 of the leading one (x2w0, x1w1, x0w2, x1w0, x0w1, x0w0)
+// in the fp32 accumulator. The dropped terms are <= 3 * 2^-24 relative; measured GEMM error
+// (tests/test_gpu_mlp.py) is at or below the exact-f32 MFMA's. Weights are split once at load
+// (host, exact); activations are split in each layer's epilogue (v_cvt_pk_bf16_f32 + subtractions)
+// and stored in LDS as three bf16 planes.
+//
+// Net and conditioning as in mlp_sampler.hip. This variant takes a context shared by all candidates
+// (mpc_step's case: one measured state per control step) or none; the time part, the Linear bias
+// and the shared context part of every cond_mlp are pre-summed into the accumulator init per step
+// (TPC: context rows, TPU: masked rows). Per-candidate contexts use the exact-f32 kernel.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include "internal.h"
+#include "mlp_common.h"
+
+namespace {
+using namespace mlpc;
+
+constexpr int ROWS = 32;
+constexpr int THREADS = 256;
+enum { SPLIT = 0, PAIRED = 1 };
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// two fp32 -> two bf16 (round to nearest even), packed: v_cvt_pk_bf16_f32
+MPCD_DEV uint32_t pk_bf16(float lo, float hi)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, bf16x2));
+}
+MPCD_DEV float bf_lo(uint32_t p) { return __builtin_bit_cast(float, p << 16); }
+MPCD_DEV float bf_hi(uint32_t p) { return __builtin_bit_cast(float, p & 0xffff0000u); }
+
+// 4 consecutive fp32 features -> three bf16 planes (4 bf16 each): v = p0 + p1 + p2 (+ < 2^-27 |v|).
+// Each remainder v - bf16(v) is exact in fp32.
+MPCD_DEV void split3(const f32x4 &v, u32x2 &p0, u32x2 &p1, u32x2 &p2)
+{
+    const uint32_t a = pk_bf16(v.x, v.y), b = pk_bf16(v.z, v.w);
+    const f32x4 r = v - f32x4{bf_lo(a), bf_hi(a), bf_lo(b), bf_hi(b)};
+    const uint32_t c = pk_bf16(r.x, r.y), d = pk_bf16(r.z, r.w);
+    const f32x4 r2 = r - f32x4{bf_lo(c), bf_hi(c), bf_lo(d), bf_hi(d)};
+    p0 = u32x2{a, b};
+    p1 = u32x2{c, d};
+    p2 = u32x2{pk_bf16(r2.x, r2.y), pk_bf16(r2.z, r2.w)};
+}
+
+// ---- LDS layout (bytes). Activation buffers hold three bf16 planes of ROWS rows; a row stride of
+// 16 mod 256 bytes keeps the 16-lane groups of a ds_read_b128 conflict-free (MI355X_MICROARCH LDS
+// table: lane (q, col) reads 16 B at row col, chunk q).
+template <int D0, int NB>
+struct Lds3 {
+    static constexpr int CPW = ROWS / NB;  // candidates per workgroup
+    static constexpr int RS = 272;         // row stride, widths <= 128
+    static constexpr int RS2 = 528;        // row stride, width 256
+    static constexpr int PL = ROWS * RS, PL2 = ROWS * RS2;  // plane strides
+    static constexpr int SX = D0 + 4;      // fp32 x row stride (floats)
+    static constexpr int T1 = 0;
+    static constexpr int S1 = T1 + 3 * PL;  // also the x planes (layer-0 input) between steps
+    static constexpr int C1 = S1 + 3 * PL;
+    static constexpr int C0 = C1 + 3 * PL;
+    static constexpr int XB = C0 + 3 * PL2;                       // fp32 x [CPW][SX]
+    static constexpr int TPC = XB + CPW * SX * 4;                 // fp32 [448]: tproj + cond bias + shared cproj
+    static constexpr int TPU = TPC + COND_TOTAL * 4;              // fp32 [448]: tproj + cond bias
+    static constexpr int BIC = TPU + COND_TOTAL * 4;              // fp32 [448]: cond-layer biases
+    static constexpr int CPS = BIC + COND_TOTAL * 4;              // fp32 [448]: shared cproj (0 without context)
+    static constexpr int BI = CPS + COND_TOTAL * 4;               // fp32 all 14 biases
+    static constexpr int total = BI + Arch<D0>::btotal() * 4;
+    static_assert(D0 * 2 + 16 <= RS, "x planes fit a 272-byte row");
+
+    // layer l: input / output buffer (byte offset incl. the feature offset of a concat half) and stride
+    static constexpr int in_off(int l) {
+        constexpr int t[NLAYER] = {S1, T1, S1, T1, C1 + 128, T1, C0 + 256, T1, C0, T1, C1, T1, S1, T1};
+        return t[l];
+    }
+    static constexpr int in_rs(int l) { return (l == 6 || l == 8) ? RS2 : RS; }
+    static constexpr int in_pl(int l) { return (l == 6 || l == 8) ? PL2 : PL; }
+    static constexpr int out_off(int l) {
+        constexpr int t[NLAYER] = {T1, S1, T1, C1 + 128, T1, C0 + 256, T1, C0, T1, C1, T1, S1, T1, 0};
+        return t[l];
+    }
+    static constexpr int out_rs(int l) { return (l == 5 || l == 7) ? RS2 : RS; }
+    static constexpr int out_pl(int l) { return (l == 5 || l == 7) ? PL2 : PL; }
+};
+
+template <int N>
+constexpr int mode_for() { return N == 32 ? SPLIT : PAIRED; }
+
+constexpr int epi_of(int l) { return l == 12 ? EPI_NONE : (l % 2 == 1) ? EPI_CMISH : EPI_MISH; }
+
+// Weight fragments of one layer for this wave: [T n-tiles][KC = K/32 k-chunks][3 planes], 16 bytes
+// (8 bf16) per lane each = the A operand of one v_mfma_f32_16x16x32_bf16.
+template <int K, int N, int MODE>
+struct WFrag3 {
+    static constexpr int NT = N / 16;
+    static constexpr int T = MODE == SPLIT ? NT / 2 : (NT + 3) / 4;
+    static constexpr int KC = K / 32;
+    u32x4 v[T][KC][3];
+};
+
+template <int K, int N, int MODE>
+MPCD_DEV int ntile_of(int wave, int j)
+{
+    return MODE == SPLIT ? (wave >> 1) + 2 * j : wave + 4 * j;
+}
+
+// One wave-uniform buffer descriptor per layer; chunk (nt, kc, plane) at soffset ((nt*KC+kc)*3+p) KiB.
+template <int K, int N, int MODE>
+MPCD_DEV void load_w3(WFrag3<K, N, MODE> &f, const float *__restrict__ wp, int wave, int lane16)
+{
+    using F = WFrag3<K, N, MODE>;
+    constexpr int KC = F::KC, NT = F::NT;
+    const uint64_t a = (uint64_t)wp;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(3 * K * N * 2), 0x00020000);
+#pragma unroll
+    for (int j = 0; j < F::T; ++j) {
+        const int nt = ntile_of<K, N, MODE>(wave, j);
+        if (MODE == PAIRED && NT % 4 != 0 && nt >= NT) continue;
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                const int soff = __builtin_amdgcn_readfirstlane(((nt * KC + kc) * 3 + pl) * 1024);
+                f.v[j][kc][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
+            }
+    }
+}
+
+MPCD_DEV f32x4 mfma_bf(const u32x4 &a, const u32x4 &b, const f32x4 &c)
+{
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
+                                                   0);
+}
+
+// the six partial products of one 32-k chunk, smallest first
+MPCD_DEV f32x4 mfma_x3(const u32x4 (&w)[3], const u32x4 (&x)[3], f32x4 acc)
+{
+    acc = mfma_bf(w[2], x[0], acc);
+    acc = mfma_bf(w[1], x[1], acc);
+    acc = mfma_bf(w[0], x[2], acc);
+    acc = mfma_bf(w[1], x[0], acc);
+    acc = mfma_bf(w[0], x[1], acc);
+    acc = mfma_bf(w[0], x[0], acc);
+    return acc;
+}
+
+// activation fragment (3 planes) of row `row`, k-chunk kc: 16 bytes per plane per lane
+MPCD_DEV void load_x3(u32x4 (&x)[3], const char *base, int plane_stride)
+{
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) x[pl] = *reinterpret_cast<const u32x4 *>(base + pl * plane_stride);
+}
+
+template <int D0, int SMODE, bool CTX>
+struct MlpX3 {
+    static constexpr int NB = (SMODE == MODE_DDIM || SMODE == MODE_EPS1) ? 1 : 2;
+    static constexpr bool IS_DDPM = SMODE == MODE_DDPM_CFG || SMODE == MODE_DDPM_XN;
+    using A = Arch<D0>;
+    using L = Lds3<D0, NB>;
+    static constexpr int CPW = L::CPW;
+    static constexpr int QUADS = D0 / 4;
+    using FW = WFrag3<32, D0, PAIRED>;
+    static constexpr int NZT = FW::T;
+
+    // Hidden layer l. SPLIT (N = 32): wave w -> column tile (w & 1), n-tiles (w >> 1) + 2j; PAIRED
+    // (N >= 64): wave w -> n-tiles w + 4j for both column tiles (each weight fragment feeds two
+    // MFMA chains). Accumulators start from the bias, or for cond layers from TPC / TPU.
+    template <int l>
+    static MPCD_DEV void hidden(const WFrag3<A::K[l], A::N[l], mode_for<A::N[l]>()> &f, char *lds, int wave, int lane)
+    {
+        constexpr int K = A::K[l], N = A::N[l], MODE = mode_for<N>(), EPI = epi_of(l);
+        using F = WFrag3<K, N, MODE>;
+        constexpr int T = F::T, KC = F::KC;
+        constexpr int NCT = MODE == SPLIT ? 1 : 2;
+        static_assert(MODE == SPLIT || N % 64 == 0, "PAIRED layers need N % 64 == 0");
+        const int col = lane & 15, q = lane >> 4;
+        const bool in_shared = l == 0 && NB == 2;  // CFG: both branches read the candidate's x
+
+        f32x4 acc[T][NCT];
+#pragma unroll
+        for (int c = 0; c < NCT; ++c) {
+            const int ct = MODE == SPLIT ? (wave & 1) : c;
+            const float *init = reinterpret_cast<const float *>(
+                lds + (EPI == EPI_CMISH ? ((NB == 2 && ct == 1) ? L::TPU : L::TPC) + cond_off(l / 2) * 4
+                                        : L::BI + A::boff(l) * 4));
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+                acc[j][c] = *reinterpret_cast<const f32x4 *>(init + ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q);
+        }
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+#pragma unroll
+            for (int c = 0; c < NCT; ++c) {
+                const int ct = MODE == SPLIT ? (wave & 1) : c;
+                const int row = in_shared ? col : ct * 16 + col;
+                u32x4 x[3];
+                load_x3(x, lds + L::in_off(l) + row * L::in_rs(l) + (kc * 32 + 8 * q) * 2, L::in_pl(l));
+#pragma unroll
+                for (int j = 0; j < T; ++j) acc[j][c] = mfma_x3(f.v[j][kc], x, acc[j][c]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < T; ++j)
+#pragma unroll
+            for (int c = 0; c < NCT; ++c) {
+                const int ct = MODE == SPLIT ? (wave & 1) : c;
+                const int n = ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q;
+                f32x4 v = acc[j][c];
+                if (EPI != EPI_NONE) {
+                    v.x = mish(v.x);
+                    v.y = mish(v.y);
+                    v.z = mish(v.z);
+                    v.w = mish(v.w);
+                }
+                u32x2 p0, p1, p2;
+                split3(v, p0, p1, p2);
+                char *o = lds + L::out_off(l) + (ct * 16 + col) * L::out_rs(l) + n * 2;
+                *reinterpret_cast<u32x2 *>(o) = p0;
+                *reinterpret_cast<u32x2 *>(o + L::out_pl(l)) = p1;
+                *reinterpret_cast<u32x2 *>(o + 2 * L::out_pl(l)) = p2;
+            }
+    }
+
+    // x (4 features) -> fp32 row in XB and the three bf16 planes layer 0 reads
+    static MPCD_DEV void store_x(char *lds, int cl, int n, const f32x4 &x)
+    {
+        *reinterpret_cast<f32x4 *>(lds + L::XB + (cl * L::SX + n) * 4) = x;
+        u32x2 p0, p1, p2;
+        split3(x, p0, p1, p2);
+        char *o = lds + L::S1 + cl * L::RS + n * 2;
+        *reinterpret_cast<u32x2 *>(o) = p0;
+        *reinterpret_cast<u32x2 *>(o + L::PL) = p1;
+        *reinterpret_cast<u32x2 *>(o + 2 * L::PL) = p2;
+    }
+
+    // final Linear (32 -> D0) + the denoise update (reference op order, see mlp_sampler.hip)
+    static MPCD_DEV void final_and_update(const FW &f, char *lds, const MlpSampleArgs &p, const StepPlan &sp, int s,
+                                          int64_t cand0, const f32x4 (&nz)[NZT][NB], int wave, int lane)
+    {
+        constexpr int T = FW::T, NT = D0 / 16;
+        const int col = lane & 15, q = lane >> 4;
+        const float *bias = reinterpret_cast<const float *>(lds + L::BI + A::boff(13) * 4);
+        f32x4 acc[T][2];
+#pragma unroll
+        for (int j = 0; j < T; ++j) {  // idle tiles (D0 = 32, waves 2-3) read n-tile 0, unused
+            const int nt = (NT % 4 == 0 || wave + 4 * j < NT) ? wave + 4 * j : 0;
+            acc[j][0] = acc[j][1] = *reinterpret_cast<const f32x4 *>(bias + nt * 16 + 4 * q);
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            u32x4 x[3];
+            load_x3(x, lds + L::T1 + (c * 16 + col) * L::RS + 8 * q * 2, L::PL);
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+                if (NT % 4 == 0 || wave + 4 * j < NT) acc[j][c] = mfma_x3(f.v[j][0], x, acc[j][c]);
+        }
+        const bool last = s == p.n_steps - 1;
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            const int nt = wave + 4 * j;
+            if (NT % 4 != 0 && nt >= NT) continue;
+            const int n = nt * 16 + 4 * q;
+#pragma unroll
+            for (int g = 0; g < (NB == 2 ? 1 : 2); ++g) {
+                // NB == 2: one candidate per lane column, eps_c = tile 0, eps_u = tile 1
+                // NB == 1: column tile g holds candidates 16g..16g+15
+                const int cl = NB == 2 ? col : g * 16 + col;
+                const f32x4 ec = acc[j][NB == 2 ? 0 : g];
+                const f32x4 eu = acc[j][1];
+                const int64_t gc = cand0 + cl;
+                if (SMODE == MODE_EPS || SMODE == MODE_EPS1) {
+                    if (gc < p.batch) {
+                        *reinterpret_cast<f32x4 *>(p.x_out + (size_t)gc * D0 + n) = ec;
+                        if (SMODE == MODE_EPS) *reinterpret_cast<f32x4 *>(p.chain + (size_t)gc * D0 + n) = eu;
+                    }
+                    continue;
+                }
+                const f32x4 x = *reinterpret_cast<const f32x4 *>(lds + L::XB + (cl * L::SX + n) * 4);
+                f32x4 xn;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float xv = x[r];
+                    float o;
+                    if (IS_DDPM) {
+                        const float x0c = sp.a * xv - sp.b * ec[r];
+                        const float x0u = sp.a * xv - sp.b * eu[r];
+                        float x0 = p.wp1 * x0c - p.wf * x0u;
+                        x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+                        const float mean = sp.c1 * x0 + sp.c2 * xv;
+                        o = (sp.flags & PLAN_NOISE) ? mean + sp.std * nz[j][0][r] : mean;
+                    } else if (SMODE == MODE_DDIM_CFG) {
+                        float x0 = p.wp1 * (sp.a * xv - sp.b * ec[r]) - p.wf * (sp.a * xv - sp.b * eu[r]);
+                        if (p.clamp_x0) x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+                        const float e = p.wp1 * ec[r] - p.wf * eu[r];
+                        o = (sp.flags & PLAN_FINAL) ? x0 : x0 * sp.sqan + sp.cn * e;
+                    } else {  // MODE_DDIM, 3-arg net
+                        float x0 = sp.a * xv - sp.b * ec[r];
+                        if (p.clamp_x0) x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+                        o = (sp.flags & PLAN_FINAL) ? x0 : x0 * sp.sqan + sp.cn * ec[r];
+                    }
+                    xn[r] = o;
+                }
+                store_x(lds, cl, n, xn);
+                if (gc < p.batch) {
+                    if (p.chain) *reinterpret_cast<f32x4 *>(p.chain + ((size_t)(s + 1) * p.batch + gc) * D0 + n) = xn;
+                    if (last) *reinterpret_cast<f32x4 *>(p.x_out + (size_t)gc * D0 + n) = xn;
+                }
+            }
+        }
+    }
+
+    // noise of step s (slice s+1) for this lane's quads, fetched one step ahead of use
+    static MPCD_DEV void fetch_noise(f32x4 (&nz)[NZT][NB], const MlpSampleArgs &p, const StepPlan &sp, int s,
+                                     int64_t cand0, int wave, int lane)
+    {
+        constexpr int NT = D0 / 16;
+#pragma unroll
+        for (int j = 0; j < NZT; ++j)
+#pragma unroll
+            for (int g = 0; g < NB; ++g) nz[j][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (!IS_DDPM || !(sp.flags & PLAN_NOISE)) return;  // DDIM: sigma = 0
+        const int col = lane & 15, q = lane >> 4;
+#pragma unroll
+        for (int j = 0; j < NZT; ++j) {
+            const int nt = wave + 4 * j;
+            if (NT % 4 != 0 && nt >= NT) continue;
+            const int n = nt * 16 + 4 * q;
+            const int64_t gc = cand0 + col;  // DDPM-CFG: NB == 2, one candidate per column
+            if (gc >= p.batch) continue;
+            if (SMODE == MODE_DDPM_XN)
+                nz[j][0] = *reinterpret_cast<const f32x4 *>(p.noise + ((size_t)(s + 1) * p.batch + gc) * D0 + n);
+            else
+                nz[j][0] = philox_normal4(p.seed, (uint64_t)(p.global_offset + gc), (uint32_t)(s + 1), (uint32_t)(n >> 2));
+        }
+    }
+
+    static MPCD_DEV void run(const MlpSampleArgs &p)
+    {
+        extern __shared__ float lds_f[];
+        char *lds = reinterpret_cast<char *>(lds_f);
+        const int lane = threadIdx.x & 63;
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const int64_t cand0 = (int64_t)blockIdx.x * CPW;
+        int lane16 = lane * 16;
+        const float *wp = p.wpack;
+        int wofs = 0;
+        auto W = [&](int l) { return wp + wofs + A::woff3(l); };
+        float *bi = reinterpret_cast<float *>(lds + L::BI);
+        float *bic = reinterpret_cast<float *>(lds + L::BIC);
+        float *cps = reinterpret_cast<float *>(lds + L::CPS);
+
+        for (int l = 0; l < NLAYER; ++l)
+            for (int i = threadIdx.x; i < A::N[l]; i += THREADS) bi[A::boff(l) + i] = wp[A::woff3(l) + 3 * A::K[l] * A::N[l] / 2 + i];
+        for (int j = 0; j < 6; ++j)
+            for (int i = threadIdx.x; i < A::N[2 * j + 1]; i += THREADS)
+                bic[cond_off(j) + i] = wp[A::woff3(2 * j + 1) + 3 * A::K[2 * j + 1] * A::N[2 * j + 1] / 2 + i];
+        for (int i = threadIdx.x; i < COND_TOTAL; i += THREADS) cps[i] = CTX ? p.cproj[i] : 0.f;
+        // x_T (fp32 + planes)
+        for (int i = threadIdx.x; i < CPW * QUADS; i += THREADS) {
+            const int c = i / QUADS, qd = i - c * QUADS;
+            const int64_t gc = cand0 + c;
+            f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (gc < p.batch) {
+                z = p.noise ? *reinterpret_cast<const f32x4 *>(p.noise + (size_t)gc * D0 + qd * 4)
+                            : philox_normal4(p.seed, (uint64_t)(p.global_offset + gc), 0u, (uint32_t)qd);
+                if (p.chain && SMODE != MODE_EPS) *reinterpret_cast<f32x4 *>(p.chain + (size_t)gc * D0 + qd * 4) = z;
+            }
+            store_x(lds, c, qd * 4, z);
+        }
+
+        WFrag3<A::K[0], A::N[0], mode_for<A::N[0]>()> w0;
+        load_w3(w0, W(0), wave, lane16);
+        f32x4 nz[NZT][NB];
+        StepPlan sp = load_plan(p.plan, 0);
+        fetch_noise(nz, p, sp, 0, cand0, wave, lane);
+        const int tpi = threadIdx.x < COND_TOTAL / 4 ? (int)threadIdx.x : 0;
+        f32x4 tpre = reinterpret_cast<const f32x4 *>(p.tproj)[tpi];
+
+        for (int s = 0; s < p.n_steps; ++s) {
+            // launder the weight base: stops LICM hoisting every layer's weight loads out of the loop
+            asm volatile("" : "+s"(wofs), "+v"(lane16));
+            WFrag3<A::K[1], A::N[1], mode_for<A::N[1]>()> w1;
+            load_w3(w1, W(1), wave, lane16);
+            lds_barrier();
+            // this step's time projections + cond biases (+ shared context part) -> TPU / TPC
+            if (threadIdx.x < COND_TOTAL / 4) {
+                const f32x4 u = tpre + reinterpret_cast<const f32x4 *>(lds + L::BIC)[tpi];
+                reinterpret_cast<f32x4 *>(lds + L::TPU)[tpi] = u;
+                reinterpret_cast<f32x4 *>(lds + L::TPC)[tpi] = u + reinterpret_cast<const f32x4 *>(lds + L::CPS)[tpi];
+            }
+            tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 1 < p.n_steps ? s + 1 : s) * COND_TOTAL)[tpi];
+            hidden<0>(w0, lds, wave, lane);
+            WFrag3<A::K[2], A::N[2], mode_for<A::N[2]>()> w2;
+            load_w3(w2, W(2), wave, lane16);
+            lds_barrier();
+            hidden<1>(w1, lds, wave, lane);
+            WFrag3<A::K[3], A::N[3], mode_for<A::N[3]>()> w3;
+            load_w3(w3, W(3), wave, lane16);
+            lds_barrier();
+            hidden<2>(w2, lds, wave, lane);
+            WFrag3<A::K[4], A::N[4], mode_for<A::N[4]>()> w4;
+            load_w3(w4, W(4), wave, lane16);
+            lds_barrier();
+            hidden<3>(w3, lds, wave, lane);
+            WFrag3<A::K[5], A::N[5], mode_for<A::N[5]>()> w5;
+            load_w3(w5, W(5), wave, lane16);
+            lds_barrier();
+            hidden<4>(w4, lds, wave, lane);
+            WFrag3<A::K[6], A::N[6], mode_for<A::N[6]>()> w6;
+            load_w3(w6, W(6), wave, lane16);
+            lds_barrier();
+            hidden<5>(w5, lds, wave, lane);
+            WFrag3<A::K[7], A::N[7], mode_for<A::N[7]>()> w7;
+            load_w3(w7, W(7), wave, lane16);
+            lds_barrier();
+            hidden<6>(w6, lds, wave, lane);
+            WFrag3<A::K[8], A::N[8], mode_for<A::N[8]>()> w8;
+            load_w3(w8, W(8), wave, lane16);
+            lds_barrier();
+            hidden<7>(w7, lds, wave, lane);
+            WFrag3<A::K[9], A::N[9], mode_for<A::N[9]>()> w9;
+            load_w3(w9, W(9), wave, lane16);
+            lds_barrier();
+            hidden<8>(w8, lds, wave, lane);
+            WFrag3<A::K[10], A::N[10], mode_for<A::N[10]>()> w10;
+            load_w3(w10, W(10), wave, lane16);
+            lds_barrier();
+            hidden<9>(w9, lds, wave, lane);
+            WFrag3<A::K[11], A::N[11], mode_for<A::N[11]>()> w11;
+            load_w3(w11, W(11), wave, lane16);
+            lds_barrier();
+            hidden<10>(w10, lds, wave, lane);
+            WFrag3<A::K[12], A::N[12], mode_for<A::N[12]>()> w12;
+            load_w3(w12, W(12), wave, lane16);
+            lds_barrier();
+            hidden<11>(w11, lds, wave, lane);
+            FW w13;
+            load_w3(w13, W(13), wave, lane16);
+            lds_barrier();
+            hidden<12>(w12, lds, wave, lane);
+            const StepPlan cur = sp;
+            f32x4 nzc[NZT][NB];
+#pragma unroll
+            for (int j = 0; j < NZT; ++j)
+#pragma unroll
+                for (int g = 0; g < NB; ++g) nzc[j][g] = nz[j][g];
+            if (s + 1 < p.n_steps) {
+                sp = load_plan(p.plan, s + 1);
+                fetch_noise(nz, p, sp, s + 1, cand0, wave, lane);
+            }
+            // next step's layer-0 weights; unconditional (a path-dependent load count drains vmcnt(0))
+            load_w3(w0, W(0), wave, lane16);
+            lds_barrier();
+            final_and_update(w13, lds, p, cur, s, cand0, nzc, wave, lane);
+        }
+    }
+};
+
+template <int D0, int SMODE, bool CTX>
+__global__ __launch_bounds__(THREADS, 1) void mlp_x3_kernel(const MlpSampleArgs p)
+{
+    MlpX3<D0, SMODE, CTX>::run(p);
+}
+
+template <int D0, int SMODE, bool CTX>
+hipError_t launch_x3(const MlpSampleArgs &a, hipStream_t stream)
+{
+    using L = Lds3<D0, MlpX3<D0, SMODE, CTX>::NB>;
+    static_assert(L::total <= 160 * 1024, "LDS budget (160 KiB per CU)");
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&mlp_x3_kernel<D0, SMODE, CTX>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    const int64_t blocks = (a.batch + L::CPW - 1) / L::CPW;
+    hipLaunchKernelGGL((mlp_x3_kernel<D0, SMODE, CTX>), dim3((unsigned)blocks), dim3(THREADS), (size_t)L::total, stream, a);
+    return hipGetLastError();
+}
+
+template <int D0>
+hipError_t launch_x3_d0(const MlpSampleArgs &a, hipStream_t stream)
+{
+    const bool ctx = a.cproj != nullptr;
+    switch (a.mode) {
+    case MODE_DDPM_CFG:
+        if (a.noise) return ctx ? launch_x3<D0, MODE_DDPM_XN, true>(a, stream) : launch_x3<D0, MODE_DDPM_XN, false>(a, stream);
+        return ctx ? launch_x3<D0, MODE_DDPM_CFG, true>(a, stream) : launch_x3<D0, MODE_DDPM_CFG, false>(a, stream);
+    case MODE_DDIM_CFG: return ctx ? launch_x3<D0, MODE_DDIM_CFG, true>(a, stream) : launch_x3<D0, MODE_DDIM_CFG, false>(a, stream);
+    case MODE_DDIM: return ctx ? launch_x3<D0, MODE_DDIM, true>(a, stream) : launch_x3<D0, MODE_DDIM, false>(a, stream);
+    case MODE_EPS: return ctx ? launch_x3<D0, MODE_EPS, true>(a, stream) : launch_x3<D0, MODE_EPS, false>(a, stream);
+    case MODE_EPS1: return ctx ? launch_x3<D0, MODE_EPS1, true>(a, stream) : launch_x3<D0, MODE_EPS1, false>(a, stream);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+int mlp_packed_floats_x3(int d0)
+{
+    switch (d0) {
+    case 32: return Arch<32>::total3();
+    case 64: return Arch<64>::total3();
+    case 128: return Arch<128>::total3();
+    default: return -1;
+    }
+}
+
+// Split Linear l (torch weight [N][K]) into three bf16 planes (w = w0 + w1 + w2, round to nearest
+// even at each level, remainders exact) and pack them as the MFMA A operand of
+// v_mfma_f32_16x16x32_bf16: chunk (nt, kc, plane) = 64 lanes x 8 bf16, lane l holding
+// W[nt*16 + (l&15)][kc*32 + 8*(l>>4) + j], j = 0..7; then the fp32 bias [N].
+static uint16_t bf16_rne(float f)
+{
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)(u >> 16);  // inf / nan: truncate
+    const uint32_t r = u + 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(r >> 16);
+}
+static float bf16_val(uint16_t h)
+{
+    const uint32_t u = (uint32_t)h << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+void mlp_pack_weights_x3(int d0, const float *const *lin_w, const float *const *lin_b, float *out)
+{
+    const int Ks[NLAYER] = {d0, 32, 32, 64, 64, 128, 128, 128, 256, 64, 128, 32, 32, 32};
+    const int Ns[NLAYER] = {32, 32, 64, 64, 128, 128, 128, 128, 64, 64, 32, 32, 32, d0};
+    size_t o = 0;  // in floats
+    for (int l = 0; l < NLAYER; ++l) {
+        const int K = Ks[l], N = Ns[l], KC = K / 32, NT = N / 16;
+        uint16_t *pk = reinterpret_cast<uint16_t *>(out + o);
+        for (int nt = 0; nt < NT; ++nt)
+            for (int kc = 0; kc < KC; ++kc)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int j = 0; j < 8; ++j) {
+                        const float w = lin_w[l][(size_t)(nt * 16 + (lane & 15)) * K + kc * 32 + 8 * (lane >> 4) + j];
+                        const uint16_t h0 = bf16_rne(w);
+                        const float r1 = w - bf16_val(h0);
+                        const uint16_t h1 = bf16_rne(r1);
+                        const float r2 = r1 - bf16_val(h1);
+                        const uint16_t h2 = bf16_rne(r2);
+                        const uint16_t hs[3] = {h0, h1, h2};
+                        for (int pl = 0; pl < 3; ++pl)
+                            pk[(((size_t)(nt * KC + kc) * 3 + pl) * 64 + lane) * 8 + j] = hs[pl];
+                    }
+        o += (size_t)3 * K * N / 2;
+        for (int n = 0; n < N; ++n) out[o + n] = lin_b[l][n];
+        o += N;
+    }
+}
+
+hipError_t launch_mlp_x3(int d0, int nb, const MlpSampleArgs &a, hipStream_t stream)
+{
+    if ((nb == 1) != (a.mode == MODE_DDIM || a.mode == MODE_EPS1)) return hipErrorInvalidValue;
+    if (a.cproj && a.cproj_stride != 0) return hipErrorInvalidValue;  // shared context only
+    switch (d0) {
+    case 32: return launch_x3_d0<32>(a, stream);
+    case 64: return launch_x3_d0<64>(a, stream);
+    case 128: return launch_x3_d0<128>(a, stream);
+    }
+    return hipErrorInvalidValue;
+}

@@ -171,6 +171,9 @@ int check_desc(const mpcd_net_desc *d)
         return fail(MPCD_EINVAL, "bad net dims");
     for (int i = 0; i < d->n_mults; ++i)
         if (d->mults[i] < 1) return fail(MPCD_EINVAL, "bad dim_mults");
+    if (d->dtype == MPCD_F16) return fail(MPCD_EUNSUP, "fp16 hidden activations are not built");
+    if (d->dtype == MPCD_F32X3 && d->kind != MPCD_NET_MLP) return fail(MPCD_EUNSUP, "MPCD_F32X3 is MLP-only");
+    if (d->dtype != MPCD_F32 && d->dtype != MPCD_F32X3) return fail(MPCD_EINVAL, "bad dtype %d", d->dtype);
     return MPCD_OK;
 }
 
@@ -204,7 +207,8 @@ struct mpcd_ctx {
     mpcd_net_desc desc{};
     int cond_dim = 0, cond_total = 0, n_cond = 0;
     DevBuf params;      // raw blob (time MLP, cond layers, UNet tensors)
-    DevBuf wpack;       // MLP packed linear layers
+    DevBuf wpack;       // MLP packed linear layers (fp32 MFMA operand order)
+    DevBuf wpack3;      // MLP linear layers split into three bf16 planes (MPCD_F32X3)
     DevBuf cond_layers; // CondLayer[n_cond]
     UnetWeights unet{}; // device pointers into `params` + repacked conv weights
     DevBuf unet_pack;
@@ -366,6 +370,12 @@ int upload_net(mpcd_ctx *c, const mpcd_net_desc &d, const float *blob, size_t n_
         rc = c->wpack.ensure(packed.size() * sizeof(float));
         if (rc) return rc;
         HIP_TRY(hipMemcpy(c->wpack.p, packed.data(), packed.size() * sizeof(float), hipMemcpyHostToDevice));
+        if (d.dtype == MPCD_F32X3) {
+            std::vector<float> packed3((size_t)mlp_packed_floats_x3(d0));
+            mlp_pack_weights_x3(d0, lw, lb, packed3.data());
+            if ((rc = c->wpack3.ensure(packed3.size() * sizeof(float)))) return rc;
+            HIP_TRY(hipMemcpy(c->wpack3.p, packed3.data(), packed3.size() * sizeof(float), hipMemcpyHostToDevice));
+        }
     } else {
         rc = unet_prepare(d, spec.size(), [&](const char *n) -> const float * {
             const int i = find(n);
@@ -387,6 +397,21 @@ int upload_net(mpcd_ctx *c, const mpcd_net_desc &d, const float *blob, size_t n_
     return MPCD_OK;
 }
 
+}  // namespace
+
+namespace {
+// MLP kernel choice: the split-bf16 kernel when the net asks for it and the context is shared (or
+// absent), else the exact-f32 kernel. Both are GPU kernels with fp32-level results.
+hipError_t launch_mlp(mpcd_ctx *c, MlpSampleArgs &m, int nb, hipStream_t st)
+{
+    const int d0 = c->desc.horizon * c->desc.state_dim;
+    if (c->desc.dtype == MPCD_F32X3 && (m.cproj == nullptr || m.cproj_stride == 0)) {
+        m.wpack = c->wpack3.as<float>();
+        return launch_mlp_x3(d0, nb, m, st);
+    }
+    m.wpack = c->wpack.as<float>();
+    return launch_mlp_sampler(d0, nb, m, st);
+}
 }  // namespace
 
 extern "C" {
@@ -445,7 +470,7 @@ void mpcd_destroy(mpcd_ctx *c)
 {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    for (DevBuf *b : {&c->params, &c->wpack, &c->cond_layers, &c->unet_pack, &c->plan, &c->tproj, &c->cproj, &c->flag,
+    for (DevBuf *b : {&c->params, &c->wpack, &c->wpack3, &c->cond_layers, &c->unet_pack, &c->plan, &c->tproj, &c->cproj, &c->flag,
                       &c->unet_ws})
         b->release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -552,7 +577,7 @@ int mpcd_sample(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr)
         m.clamp_x0 = a->clamp_x0;
         m.wp1 = wp1;
         m.wf = wf;
-        HIP_TRY(launch_mlp_sampler(d.horizon * d.state_dim, cfg ? 2 : 1, m, st));
+        HIP_TRY(launch_mlp(c, m, cfg ? 2 : 1, st));
     } else {
         UnetSampleArgs u{};
         u.plan = c->plan.as<StepPlan>();
@@ -650,7 +675,7 @@ int mpcd_eps(mpcd_ctx *c, const float *x, int32_t t, const float *context, int32
     m.n_steps = 1;
     m.mode = cfg ? MODE_EPS : MODE_EPS1;
     m.dbg = c->dbg;
-    HIP_TRY(launch_mlp_sampler(d.horizon * d.state_dim, cfg ? 2 : 1, m, st));
+    HIP_TRY(launch_mlp(c, m, cfg ? 2 : 1, st));
     return MPCD_OK;
 }
 

@@ -41,6 +41,8 @@ class NetSpec:
     dim_mults: tuple = (1, 2, 4)
     time_emb_dim: int = 32
     cfg: bool = True          # 4-arg net with the CFG context mask
+    # GEMM numerics: "f32" exact fp32 MFMA; "f32x3" fp32-accurate split-bf16 MFMA (MLP, shared or no
+    # context; include/mpcd.h MPCD_F32X3); "f16" not built
     dtype: str = "f32"
 
     def desc(self):
@@ -52,7 +54,10 @@ class NetSpec:
             d.mults[i] = m
         d.time_emb_dim = self.time_emb_dim
         d.cfg_masked = 1 if self.cfg else 0
-        d.dtype = N.MPCD_F16 if self.dtype == "f16" else N.MPCD_F32
+        dtypes = {"f32": N.MPCD_F32, "f16": N.MPCD_F16, "f32x3": N.MPCD_F32X3}
+        if self.dtype not in dtypes:
+            raise ValueError(f"dtype {self.dtype!r}: use one of {sorted(dtypes)}")
+        d.dtype = dtypes[self.dtype]
         return d
 
 

@@ -1,4 +1,6 @@
-"""GPU parity: persistent MLP sampler (CFG-DDPM, CFG-DDIM, DDIM) against the oracle, via the C ABI."""
+"""GPU parity: persistent MLP sampler (CFG-DDPM, CFG-DDIM, DDIM) against the oracle, via the C ABI.
+Every test runs both GEMM numerics: "f32" (exact fp32 MFMA) and "f32x3" (split-bf16 MFMA), at the
+same tolerances."""
 import numpy as np
 import pytest
 import torch
@@ -12,8 +14,13 @@ from ._util import assert_traj_close, make_mlp, oracle_sensitivity
 pytestmark = pytest.mark.gpu
 
 
-def _planner(net, d, H, C, n_steps=100, kind="exponential", cfg=True):
-    spec = NetSpec("mlp", state_dim=d, horizon=H, context_dim=C, cfg=cfg)
+@pytest.fixture(params=["f32", "f32x3"])
+def dtype(request):
+    return request.param
+
+
+def _planner(net, d, H, C, n_steps=100, kind="exponential", cfg=True, dtype="f32"):
+    spec = NetSpec("mlp", state_dim=d, horizon=H, context_dim=C, cfg=cfg, dtype=dtype)
     return DiffusionMPC(spec, net.state_dict(), variance_schedule=kind, n_diffusion_steps=n_steps)
 
 
@@ -29,9 +36,9 @@ def _ctx(B, C, shared, seed=3):
     (100, 32, 2, 4, 100, 5, False),  # ragged batch (not a multiple of 16), per-candidate context, nwo > 0
     (48, 64, 2, 3, 25, 3, False),    # H*d = 128
 ])
-def test_ddpm_cfg_matches_oracle(B, H, d, C, N, nwo, shared):
+def test_ddpm_cfg_matches_oracle(B, H, d, C, N, nwo, shared, dtype):
     net = make_mlp(d, H, C)
-    plan = _planner(net, d, H, C, N)
+    plan = _planner(net, d, H, C, N, dtype=dtype)
     ctx = _ctx(B, C, shared)
     S = N + nwo
     noise = torch.randn(S + 1, B, H, d, generator=torch.Generator().manual_seed(11))
@@ -45,10 +52,10 @@ def test_ddpm_cfg_matches_oracle(B, H, d, C, N, nwo, shared):
     assert_traj_close(got, ref, what="ddpm chain")
 
 
-def test_ddpm_cfg_cosine_250():
+def test_ddpm_cfg_cosine_250(dtype):
     B, H, d, C, N = 32, 32, 2, 4, 250
     net = make_mlp(d, H, C, seed=5)
-    plan = _planner(net, d, H, C, N, kind="cosine")
+    plan = _planner(net, d, H, C, N, kind="cosine", dtype=dtype)
     ctx = _ctx(B, C, True)
     noise = torch.randn(N + 1, B, H, d, generator=torch.Generator().manual_seed(2))
     ref = osam.ddpm_cfg(net, osch.buffers("cosine", N), ctx.expand(B, C), 0.01, B, H, noise=noise)
@@ -57,10 +64,10 @@ def test_ddpm_cfg_cosine_250():
 
 
 @pytest.mark.parametrize("steps,clamp", [(None, False), (20, True)])
-def test_ddim_cfg_matches_oracle(steps, clamp):
+def test_ddim_cfg_matches_oracle(steps, clamp, dtype):
     B, H, d, C, N = 64, 32, 2, 4, 100
     net = make_mlp(d, H, C, seed=2)
-    plan = _planner(net, d, H, C, N)
+    plan = _planner(net, d, H, C, N, dtype=dtype)
     ctx = _ctx(B, C, True)
     S = len(osam.ddim_grid(N, steps))
     noise = torch.randn(S + 1, B, H, d, generator=torch.Generator().manual_seed(4))
@@ -72,11 +79,11 @@ def test_ddim_cfg_matches_oracle(steps, clamp):
     assert_traj_close(got[: ref.shape[0]], ref, abs_elem=max(1e-4, 4 * spread), what="ddim_cfg chain")
 
 
-def test_ddim_uncond_matches_oracle():
+def test_ddim_uncond_matches_oracle(dtype):
     """3-arg net (context concatenated, no mask) + reference ddim_sample (unclamped)."""
     B, H, d, C, N = 64, 32, 2, 4, 100
     net = make_mlp(d, H, C, seed=6)
-    plan = _planner(net, d, H, C, N, cfg=False)
+    plan = _planner(net, d, H, C, N, cfg=False, dtype=dtype)
     ctx = _ctx(B, C, False)
     S = len(osam.ddim_grid(N))
     noise = torch.randn(S + 1, B, H, d, generator=torch.Generator().manual_seed(8))
@@ -89,11 +96,11 @@ def test_ddim_uncond_matches_oracle():
     assert_traj_close(got, ref, abs_elem=max(1e-4, 4 * spread), what="ddim")
 
 
-def test_eps_forward_both_branches():
+def test_eps_forward_both_branches(dtype):
     """One net forward (A11) on both CFG branches vs the oracle, every layer path."""
     B, H, d, C, N = 40, 32, 2, 4, 100
     net = make_mlp(d, H, C, seed=12)
-    plan = _planner(net, d, H, C, N)
+    plan = _planner(net, d, H, C, N, dtype=dtype)
     x = torch.randn(B, H, d, generator=torch.Generator().manual_seed(1))
     for shared in (True, False):
         ctx = _ctx(B, C, shared)
@@ -107,11 +114,11 @@ def test_eps_forward_both_branches():
             assert float((eu.cpu() - ru).abs().max()) < 5e-6
 
 
-def test_philox_shard_invariance_and_stats():
+def test_philox_shard_invariance_and_stats(dtype):
     """Throughput mode: noise keyed by global candidate index -> identical results for any sharding."""
     B, H, d, C, N = 512, 32, 2, 4, 100
     net = make_mlp(d, H, C)
-    plan = _planner(net, d, H, C, N)
+    plan = _planner(net, d, H, C, N, dtype=dtype)
     ctx = _ctx(B, C, True)
     full = plan.sample_trajectories(ctx, B, H, seed=123, return_chain=True)
     a = plan.sample_trajectories(ctx, B // 2, H, seed=123, global_offset=0, return_chain=True)
@@ -126,11 +133,11 @@ def test_philox_shard_invariance_and_stats():
     assert not torch.equal(full[-1], other)
 
 
-def test_full_size_cfg2_properties():
+def test_full_size_cfg2_properties(dtype):
     """BASELINE cfg 2 size (B=4096, H=32, N=100): finite, inside the clamp bound, deterministic."""
     B, H, d, C, N = 4096, 32, 2, 4, 100
     net = make_mlp(d, H, C)
-    plan = _planner(net, d, H, C, N)
+    plan = _planner(net, d, H, C, N, dtype=dtype)
     ctx = _ctx(B, C, True)
     x1 = plan.sample_trajectories(ctx, B, H, seed=7)
     x2 = plan.sample_trajectories(ctx, B, H, seed=7)
@@ -142,3 +149,16 @@ def test_full_size_cfg2_properties():
     # a 64-candidate slice equals the same candidates run alone (shard property at full size)
     part = plan.sample_trajectories(ctx, 64, H, seed=7, global_offset=4032)
     assert torch.equal(part, x1[4032:])
+
+
+def test_f32x3_matches_exact_f32_at_full_size():
+    """cfg 2 size, Philox noise: the split-bf16 kernel against the exact-f32 kernel (same seed)."""
+    B, H, d, C, N = 4096, 32, 2, 4, 100
+    net = make_mlp(d, H, C, seed=21)
+    ctx = _ctx(B, C, True)
+    a = _planner(net, d, H, C, N, dtype="f32").sample_trajectories(ctx, B, H, seed=9)
+    b = _planner(net, d, H, C, N, dtype="f32x3").sample_trajectories(ctx, B, H, seed=9)
+    torch.cuda.synchronize()
+    assert torch.isfinite(b).all()
+    rel = (a - b).flatten(1).norm(dim=1) / a.flatten(1).norm(dim=1).clamp_min(1e-12)
+    assert float(rel.max()) < 1e-4, float(rel.max())
