@@ -26,8 +26,12 @@ sys.path.insert(0, ROOT)
 CFG = dict(workload="cfg2: 2D double integrator, MLP noise-net, CFG-DDPM", system="double_int2d", d=2, H=32, C=4,
            N=100, B=4096, w=0.01, schedule="exponential")
 MAC_FWD = 119552          # MLP MACs per forward at H*d = 64 (incl. time MLP + cond projections)
+MAC_ROW = 95232           # MACs the kernel executes per row and step: the 14 per-row Linears (time MLP and
+                          # cond projections run once per step / per context in the prologues)
 PEAK_FP32 = 157.3e12      # MI355X dense fp32 MFMA / vector peak, FLOP/s (MI355X_MICROARCH.md)
-PMC_FILE = os.path.join(ROOT, "profiles", "r1_pmc_mlp_sampler.json")
+PEAK_BF16 = 2516.6e12     # MI355X dense bf16 MFMA peak: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz
+PMC_FILES = {"f32": os.path.join(ROOT, "profiles", "r1_pmc_mlp_sampler.json"),
+             "f32x3": os.path.join(ROOT, "profiles", "r1_pmc_mlp_x3.json")}
 
 
 def _rank_env():
@@ -120,11 +124,24 @@ def main():
 
     if rank == 0:
         total = CFG["B"] * world * args.steps
-        flops_launch = CFG["B"] * CFG["N"] * 2 * 2 * MAC_FWD
+        flops_launch = CFG["B"] * CFG["N"] * 2 * 2 * MAC_FWD   # survey's algorithmic count (fp32 FLOPs)
         achieved = flops_launch / (kms * 1e-3)
+        if args.dtype == "f32x3":
+            # executed matrix-core work: six bf16 partial products per fp32 MAC of the per-row Linears
+            mfma_flops = CFG["B"] * 2 * CFG["N"] * MAC_ROW * 2 * 6
+            roof = {"bound": "mfma", "achieved": mfma_flops / (kms * 1e-3) / 1e12, "peak": PEAK_BF16 / 1e12,
+                    "unit": "TFLOP/s", "frac": mfma_flops / (kms * 1e-3) / PEAK_BF16,
+                    "peak_note": "bf16 dense MFMA peak; the kernel computes fp32-accurate GEMMs as 3-way bf16 splits",
+                    "fp32_equiv": {"achieved": achieved / 1e12, "peak": PEAK_FP32 / 1e12,
+                                   "frac": achieved / PEAK_FP32, "flop_per_launch": flops_launch},
+                    "kernel": "mlp_x3_kernel<64,DDPM_CFG,ctx>", "flop_per_launch": mfma_flops}
+        else:
+            roof = {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP32 / 1e12, "unit": "TFLOP/s",
+                    "frac": achieved / PEAK_FP32, "kernel": "mlp_sample_kernel<64,DDPM_CFG,ctx>",
+                    "flop_per_launch": flops_launch}
         traffic = None
-        if os.path.exists(PMC_FILE):
-            with open(PMC_FILE) as f:
+        if os.path.exists(PMC_FILES[args.dtype]):
+            with open(PMC_FILES[args.dtype]) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
         out = {
             "metric": "candidate trajectories/sec (100 denoise steps, H=32)",
@@ -141,11 +158,11 @@ def main():
             "data": "synthetic (random-init weights seed 0, x0 ~ U[-1,1]^4, Philox noise)",
             "config": {"workload": CFG["workload"], "candidates_per_gpu": CFG["B"], "horizon": CFG["H"],
                        "action_dim": CFG["d"], "context_dim": CFG["C"], "denoise_steps": CFG["N"],
-                       "sampler": "CFG-DDPM w=0.01", "schedule": CFG["schedule"], "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP32 / 1e12, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP32, "traffic": traffic,
-                         "kernel": "mlp_sample_kernel<64,DDPM_CFG,ctx>", "kernel_ms": kms,
-                         "flop_per_launch": flops_launch},
+                       "sampler": "CFG-DDPM w=0.01", "schedule": CFG["schedule"], "parallelism": f"dp{world}",
+                       "gemm": {"f32": "exact fp32 MFMA (v_mfma_f32_16x16x4_f32)",
+                                "f32x3": "fp32-accurate split-bf16 MFMA (3 bf16 terms per operand, 6 partial "
+                                         "products, fp32 accumulate)"}[args.dtype]},
+            "roofline": dict(roof, traffic=traffic, kernel_ms=kms),
             "best_cost_last_step": r.best_cost,
         }
         if world == 1 and not args.no_cpu_baseline:

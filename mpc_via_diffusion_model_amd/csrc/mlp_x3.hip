@@ -193,6 +193,16 @@ struct MlpX3 {
         const int col = lane & 15, q = lane >> 4;
         const bool in_shared = l == 0 && NB == 2;  // CFG: both branches read the candidate's x
 
+        // activation fragments of both column tiles over the whole K, read up front
+        u32x4 x[NCT][KC][3];
+#pragma unroll
+        for (int c = 0; c < NCT; ++c) {
+            const int ct = MODE == SPLIT ? (wave & 1) : c;
+            const int row = in_shared ? col : ct * 16 + col;
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc)
+                load_x3(x[c][kc], lds + L::in_off(l) + row * L::in_rs(l) + (kc * 32 + 8 * q) * 2, L::in_pl(l));
+        }
         f32x4 acc[T][NCT];
 #pragma unroll
         for (int c = 0; c < NCT; ++c) {
@@ -204,38 +214,55 @@ struct MlpX3 {
             for (int j = 0; j < T; ++j)
                 acc[j][c] = *reinterpret_cast<const f32x4 *>(init + ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q);
         }
+        // Output tiles in G groups (T = 2: the n-tiles; else the column tiles); group g's MFMAs are
+        // issued together with group g-1's epilogue: a bf16 MFMA leaves the SIMD's vector issue free
+        // for 8 of its 16 cycles (unlike the f32 MFMA), so the Mish / split VALU rides in its shadow.
+        constexpr bool BYJ = T == 2;
+        constexpr int G = BYJ ? T : NCT;
+        auto tile_mfma = [&](int j, int c) {
 #pragma unroll
-        for (int kc = 0; kc < KC; ++kc) {
-#pragma unroll
-            for (int c = 0; c < NCT; ++c) {
-                const int ct = MODE == SPLIT ? (wave & 1) : c;
-                const int row = in_shared ? col : ct * 16 + col;
-                u32x4 x[3];
-                load_x3(x, lds + L::in_off(l) + row * L::in_rs(l) + (kc * 32 + 8 * q) * 2, L::in_pl(l));
-#pragma unroll
-                for (int j = 0; j < T; ++j) acc[j][c] = mfma_x3(f.v[j][kc], x, acc[j][c]);
+            for (int kc = 0; kc < KC; ++kc) acc[j][c] = mfma_x3(f.v[j][kc], x[c][kc], acc[j][c]);
+        };
+        auto tile_epi = [&](int j, int c) {
+            const int ct = MODE == SPLIT ? (wave & 1) : c;
+            const int n = ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q;
+            f32x4 v = acc[j][c];
+            if (EPI != EPI_NONE) {
+                v.x = mish(v.x);
+                v.y = mish(v.y);
+                v.z = mish(v.z);
+                v.w = mish(v.w);
             }
+            u32x2 p0, p1, p2;
+            split3(v, p0, p1, p2);
+            char *o = lds + L::out_off(l) + (ct * 16 + col) * L::out_rs(l) + n * 2;
+            *reinterpret_cast<u32x2 *>(o) = p0;
+            *reinterpret_cast<u32x2 *>(o + L::out_pl(l)) = p1;
+            *reinterpret_cast<u32x2 *>(o + 2 * L::out_pl(l)) = p2;
+        };
+        auto group = [&](int g, bool epi) {
+#pragma unroll
+            for (int i = 0; i < (BYJ ? NCT : 1); ++i) {
+                const int j = BYJ ? g : 0, c = BYJ ? i : g;
+                if (epi) tile_epi(j, c); else tile_mfma(j, c);
+            }
+        };
+        // MFMAs per group, and ~3 VALU of the previous group's epilogue per MFMA
+        constexpr int NM = (BYJ ? NCT : 1) * KC * 6;
+        group(0, false);
+#pragma unroll
+        for (int g = 1; g < G; ++g) {
+            __builtin_amdgcn_sched_barrier(0);
+            group(g, false);
+            group(g - 1, true);
+#pragma unroll
+            for (int i = 0; i < NM; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // 3 VALU
+            }
+            __builtin_amdgcn_sched_barrier(0);
         }
-#pragma unroll
-        for (int j = 0; j < T; ++j)
-#pragma unroll
-            for (int c = 0; c < NCT; ++c) {
-                const int ct = MODE == SPLIT ? (wave & 1) : c;
-                const int n = ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q;
-                f32x4 v = acc[j][c];
-                if (EPI != EPI_NONE) {
-                    v.x = mish(v.x);
-                    v.y = mish(v.y);
-                    v.z = mish(v.z);
-                    v.w = mish(v.w);
-                }
-                u32x2 p0, p1, p2;
-                split3(v, p0, p1, p2);
-                char *o = lds + L::out_off(l) + (ct * 16 + col) * L::out_rs(l) + n * 2;
-                *reinterpret_cast<u32x2 *>(o) = p0;
-                *reinterpret_cast<u32x2 *>(o + L::out_pl(l)) = p1;
-                *reinterpret_cast<u32x2 *>(o + 2 * L::out_pl(l)) = p2;
-            }
+        group(G - 1, true);
     }
 
     // x (4 features) -> fp32 row in XB and the three bf16 planes layer 0 reads
@@ -393,12 +420,28 @@ struct MlpX3 {
         const int tpi = threadIdx.x < COND_TOTAL / 4 ? (int)threadIdx.x : 0;
         f32x4 tpre = reinterpret_cast<const f32x4 *>(p.tproj)[tpi];
 
+#ifdef MPCD_PROF_LAYERS
+        // experiment build only: per-wave shader-clock cycles of each layer (work, then barrier wait)
+        uint64_t tacc[2 * 16] = {};
+        const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+        uint64_t tprev = __builtin_readcyclecounter();
+        const uint64_t ct0 = tprev;
+        auto bar = [&](int k) {
+            uint64_t t = __builtin_readcyclecounter();
+            tacc[2 * k] += t - tprev;
+            lds_barrier();
+            tprev = __builtin_readcyclecounter();
+            tacc[2 * k + 1] += tprev - t;
+        };
+#else
+        auto bar = [](int) { lds_barrier(); };
+#endif
         for (int s = 0; s < p.n_steps; ++s) {
             // launder the weight base: stops LICM hoisting every layer's weight loads out of the loop
             asm volatile("" : "+s"(wofs), "+v"(lane16));
             WFrag3<A::K[1], A::N[1], mode_for<A::N[1]>()> w1;
             load_w3(w1, W(1), wave, lane16);
-            lds_barrier();
+            bar(0);
             // this step's time projections + cond biases (+ shared context part) -> TPU / TPC
             if (threadIdx.x < COND_TOTAL / 4) {
                 const f32x4 u = tpre + reinterpret_cast<const f32x4 *>(lds + L::BIC)[tpi];
@@ -409,51 +452,51 @@ struct MlpX3 {
             hidden<0>(w0, lds, wave, lane);
             WFrag3<A::K[2], A::N[2], mode_for<A::N[2]>()> w2;
             load_w3(w2, W(2), wave, lane16);
-            lds_barrier();
+            bar(1);
             hidden<1>(w1, lds, wave, lane);
             WFrag3<A::K[3], A::N[3], mode_for<A::N[3]>()> w3;
             load_w3(w3, W(3), wave, lane16);
-            lds_barrier();
+            bar(2);
             hidden<2>(w2, lds, wave, lane);
             WFrag3<A::K[4], A::N[4], mode_for<A::N[4]>()> w4;
             load_w3(w4, W(4), wave, lane16);
-            lds_barrier();
+            bar(3);
             hidden<3>(w3, lds, wave, lane);
             WFrag3<A::K[5], A::N[5], mode_for<A::N[5]>()> w5;
             load_w3(w5, W(5), wave, lane16);
-            lds_barrier();
+            bar(4);
             hidden<4>(w4, lds, wave, lane);
             WFrag3<A::K[6], A::N[6], mode_for<A::N[6]>()> w6;
             load_w3(w6, W(6), wave, lane16);
-            lds_barrier();
+            bar(5);
             hidden<5>(w5, lds, wave, lane);
             WFrag3<A::K[7], A::N[7], mode_for<A::N[7]>()> w7;
             load_w3(w7, W(7), wave, lane16);
-            lds_barrier();
+            bar(6);
             hidden<6>(w6, lds, wave, lane);
             WFrag3<A::K[8], A::N[8], mode_for<A::N[8]>()> w8;
             load_w3(w8, W(8), wave, lane16);
-            lds_barrier();
+            bar(7);
             hidden<7>(w7, lds, wave, lane);
             WFrag3<A::K[9], A::N[9], mode_for<A::N[9]>()> w9;
             load_w3(w9, W(9), wave, lane16);
-            lds_barrier();
+            bar(8);
             hidden<8>(w8, lds, wave, lane);
             WFrag3<A::K[10], A::N[10], mode_for<A::N[10]>()> w10;
             load_w3(w10, W(10), wave, lane16);
-            lds_barrier();
+            bar(9);
             hidden<9>(w9, lds, wave, lane);
             WFrag3<A::K[11], A::N[11], mode_for<A::N[11]>()> w11;
             load_w3(w11, W(11), wave, lane16);
-            lds_barrier();
+            bar(10);
             hidden<10>(w10, lds, wave, lane);
             WFrag3<A::K[12], A::N[12], mode_for<A::N[12]>()> w12;
             load_w3(w12, W(12), wave, lane16);
-            lds_barrier();
+            bar(11);
             hidden<11>(w11, lds, wave, lane);
             FW w13;
             load_w3(w13, W(13), wave, lane16);
-            lds_barrier();
+            bar(12);
             hidden<12>(w12, lds, wave, lane);
             const StepPlan cur = sp;
             f32x4 nzc[NZT][NB];
@@ -467,9 +510,25 @@ struct MlpX3 {
             }
             // next step's layer-0 weights; unconditional (a path-dependent load count drains vmcnt(0))
             load_w3(w0, W(0), wave, lane16);
-            lds_barrier();
+            bar(13);
             final_and_update(w13, lds, p, cur, s, cand0, nzc, wave, lane);
         }
+#ifdef MPCD_PROF_LAYERS
+        {
+            const uint64_t t = __builtin_readcyclecounter();
+            tacc[2 * 15] += t - tprev;
+            if (p.dbg && blockIdx.x < 8 && lane == 0)
+                for (int i = 0; i < 32; ++i) p.dbg[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + i] = (float)tacc[i];
+            if (p.dbg && threadIdx.x == 0) {  // per-block loop start / end (memrealtime, low 32 bits)
+                p.dbg[4096 + blockIdx.x * 2] = __builtin_bit_cast(float, (uint32_t)rt0);
+                p.dbg[4096 + blockIdx.x * 2 + 1] = __builtin_bit_cast(float, (uint32_t)__builtin_amdgcn_s_memrealtime());
+            }
+            if (p.dbg && blockIdx.x < 8 && threadIdx.x == 0) {  // shader clock = d(memtime) / d(memrealtime) x 100 MHz
+                p.dbg[8 * 4 * 32 + blockIdx.x * 2] = (float)(t - ct0);
+                p.dbg[8 * 4 * 32 + blockIdx.x * 2 + 1] = (float)(__builtin_amdgcn_s_memrealtime() - rt0);
+            }
+        }
+#endif
     }
 };
 

@@ -17,7 +17,7 @@ from oracle import nets  # noqa: E402
 
 torch.manual_seed(0)
 net = nets.ConditionedMLPNet(state_dim=2, horizon=32, context_dim=4)
-plan = DiffusionMPC(NetSpec("mlp", state_dim=2, horizon=32, context_dim=4), net.state_dict(),
+plan = DiffusionMPC(NetSpec("mlp", state_dim=2, horizon=32, context_dim=4, dtype=os.environ.get("DTYPE", "f32")), net.state_dict(),
                     variance_schedule="exponential", n_diffusion_steps=100)
 ctx = torch.rand(1, 4) * 2 - 1
 B = int(os.environ.get("B", 4096))
