@@ -175,6 +175,37 @@ typedef struct {
 int mpcd_argmin(mpcd_ctx *ctx, const double *cost, int64_t n, int64_t index_offset, mpcd_best *best_dev,
                 void *hip_stream);
 
+/* ---- Closed loop on the device: M plant states advanced together, each with its
+ * own group of `group` consecutive candidates, no host round trip inside the loop
+ * (Cart_Diffusion_inference.py:405-512 runs one state at a time on the host). */
+
+/* Per-group clip flags: flags_dev[g] = 1 iff some x in [g*group_elems, (g+1)*group_elems) leaves
+ * [-1-1e-4, 1+1e-4] (LimitsNormalizer's rule applied to each state's own candidate batch). */
+int mpcd_clip_flags(mpcd_ctx *ctx, const float *x, int64_t n_groups, int64_t group_elems, int32_t *flags_dev,
+                    void *hip_stream);
+
+/* normalize_condition of n_states device fp64 states [n_states][dim] (normalization.py:149-154 in fp64,
+ * then the net's .float()): ctx_out dev fp32 [n_states][dim]. min/max host fp32 [dim], dim <= 16. */
+int mpcd_normalize_states(mpcd_ctx *ctx, const double *x_dev, int64_t n_states, int32_t dim, const float *min_host,
+                          const float *max_host, float *ctx_out, void *hip_stream);
+
+/* mpcd_rollout_cost with one start state per group: candidate b starts from x0_dev[b / group] (dev fp64
+ * [batch/group][n_x]) and uses flags_dev[b / group]. batch % group == 0. */
+int mpcd_rollout_cost_grouped(mpcd_ctx *ctx, const mpcd_system_desc *sys, const double *x0_dev, int64_t group,
+                              const float *u_norm, const float *umin_host, const float *umax_host, int64_t batch,
+                              int32_t horizon, const int32_t *flags_dev, double *cost_out, void *hip_stream);
+
+/* One control step for n_states plant states (A15 + the plant step): for state m pick the candidate of
+ * [m*group, (m+1)*group) with the lowest cost (NaN = +inf, lowest index on ties) or, select_first != 0,
+ * the group's first one (the reference scripts' n_samples = 1 use); unnormalise its u[0] with
+ * flags_dev[m]; round it to `decimals` places (the reference's round(u, 4); < 0 = no rounding); then
+ * x_dev[m] <- f(x_dev[m], u0) in fp64 with the system's dynamics (in place). Outputs (device):
+ * u_applied [n_states][n_u] fp64, best_index [n_states] int64 (global candidate index), best_cost fp64. */
+int mpcd_control_step(mpcd_ctx *ctx, const mpcd_system_desc *sys, double *x_dev, int64_t n_states, int64_t group,
+                      const float *u_norm, int32_t horizon, const double *cost, const float *umin_host,
+                      const float *umax_host, const int32_t *flags_dev, int32_t select_first, int32_t decimals,
+                      double *u_applied, int64_t *best_index, double *best_cost, void *hip_stream);
+
 /* Timing of the last mpcd_sample's main kernel (HIP events on the call's stream), milliseconds.
  * Blocks until that kernel has finished. */
 int mpcd_last_sample_ms(mpcd_ctx *ctx, float *ms);

@@ -18,9 +18,16 @@
 hipError_t launch_clip_flag(const float *x, int64_t n, int *flag_dev, hipStream_t stream);
 hipError_t launch_unnormalize(const float *x, int64_t n, int dim, const int *flag_dev, const float *mn_host,
                               const float *mx_host, float *out, hipStream_t stream);
-hipError_t launch_rollout_cost(const mpcd_system_desc &d, const double *x0_host, const float *u_norm,
-                               const float *umin_host, const float *umax_host, const int *flag_dev, int64_t batch, int H,
-                               double *cost, hipStream_t stream);
+hipError_t launch_rollout_cost(const mpcd_system_desc &d, const double *x0_host, const double *x0_dev, int64_t group,
+                               const float *u_norm, const float *umin_host, const float *umax_host, const int *flag_dev,
+                               int64_t batch, int H, double *cost, hipStream_t stream);
+hipError_t launch_clip_flags(const float *x, int64_t n_groups, int64_t group_elems, int *flags_dev, hipStream_t stream);
+hipError_t launch_normalize_states(const double *x, int64_t M, int C, const float *mn_host, const float *mx_host,
+                                   float *out, hipStream_t stream);
+hipError_t launch_control_step(const mpcd_system_desc &d, double *x_dev, int64_t M, int64_t group, const float *u_norm,
+                               int H, const double *cost, const float *umin_host, const float *umax_host,
+                               const int *flags_dev, int select_first, int decimals, double *u_applied,
+                               int64_t *best_idx, double *best_cost, hipStream_t stream);
 hipError_t launch_argmin(const double *cost, int64_t n, int64_t offset, mpcd_best *best, hipStream_t stream);
 
 namespace {
@@ -723,7 +730,69 @@ int mpcd_rollout_cost(mpcd_ctx *c, const mpcd_system_desc *sys, const double *x0
         HIP_TRY(launch_clip_flag(u_norm, batch * horizon * sys->n_u, c->flag.as<int>(), st));
         flag = c->flag.as<int>();
     }
-    HIP_TRY(launch_rollout_cost(*sys, x0, u_norm, umin, umax, flag, batch, horizon, cost, st));
+    HIP_TRY(launch_rollout_cost(*sys, x0, nullptr, batch, u_norm, umin, umax, flag, batch, horizon, cost, st));
+    return MPCD_OK;
+}
+
+namespace {
+int check_system(const mpcd_system_desc *sys, int32_t horizon)
+{
+    if (sys->n_x < 1 || sys->n_x > 12 || sys->n_u < 1 || sys->n_u > 4) return fail(MPCD_EINVAL, "n_x/n_u");
+    if (sys->system < 0 || sys->system > MPCD_SYS_QUADROTOR12) return fail(MPCD_EINVAL, "system %d", sys->system);
+    if (sys->cost_kind == MPCD_COST_CALMPC && (sys->n_u != 1 || horizon < 3))
+        return fail(MPCD_EINVAL, "calMPCCost needs n_u == 1 and H >= 3");
+    if ((size_t)horizon * sys->n_u * 64 * sizeof(float) > 64 * 1024) return fail(MPCD_EUNSUP, "H*n_u too large");
+    return MPCD_OK;
+}
+}  // namespace
+
+int mpcd_clip_flags(mpcd_ctx *c, const float *x, int64_t n_groups, int64_t group_elems, int32_t *flags, void *stream_ptr)
+{
+    if (!c || !x || !flags) return fail(MPCD_EINVAL, "null argument");
+    if (n_groups < 1 || group_elems < 1) return fail(MPCD_EINVAL, "n_groups / group_elems");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_clip_flags(x, n_groups, group_elems, flags, static_cast<hipStream_t>(stream_ptr)));
+    return MPCD_OK;
+}
+
+int mpcd_normalize_states(mpcd_ctx *c, const double *x, int64_t n_states, int32_t dim, const float *mn,
+                          const float *mx, float *out, void *stream_ptr)
+{
+    if (!c || !x || !mn || !mx || !out) return fail(MPCD_EINVAL, "null argument");
+    if (n_states < 1 || dim < 1 || dim > 16) return fail(MPCD_EINVAL, "n_states / dim (1..16)");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_normalize_states(x, n_states, dim, mn, mx, out, static_cast<hipStream_t>(stream_ptr)));
+    return MPCD_OK;
+}
+
+int mpcd_rollout_cost_grouped(mpcd_ctx *c, const mpcd_system_desc *sys, const double *x0_dev, int64_t group,
+                              const float *u_norm, const float *umin, const float *umax, int64_t batch,
+                              int32_t horizon, const int32_t *flags, double *cost, void *stream_ptr)
+{
+    if (!c || !sys || !x0_dev || !u_norm || !umin || !umax || !flags || !cost) return fail(MPCD_EINVAL, "null argument");
+    if (batch < 1 || horizon < 2 || group < 1 || batch % group) return fail(MPCD_EINVAL, "batch/group/horizon");
+    int rc = check_system(sys, horizon);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_rollout_cost(*sys, nullptr, x0_dev, group, u_norm, umin, umax, flags, batch, horizon, cost,
+                                static_cast<hipStream_t>(stream_ptr)));
+    return MPCD_OK;
+}
+
+int mpcd_control_step(mpcd_ctx *c, const mpcd_system_desc *sys, double *x, int64_t n_states, int64_t group,
+                      const float *u_norm, int32_t horizon, const double *cost, const float *umin, const float *umax,
+                      const int32_t *flags, int32_t select_first, int32_t decimals, double *u_applied,
+                      int64_t *best_index, double *best_cost, void *stream_ptr)
+{
+    if (!c || !sys || !x || !u_norm || !cost || !umin || !umax || !flags || !u_applied || !best_index || !best_cost)
+        return fail(MPCD_EINVAL, "null argument");
+    if (n_states < 1 || group < 1 || horizon < 1) return fail(MPCD_EINVAL, "n_states/group/horizon");
+    if (decimals > 15) return fail(MPCD_EINVAL, "decimals > 15");
+    int rc = check_system(sys, horizon);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_control_step(*sys, x, n_states, group, u_norm, horizon, cost, umin, umax, flags, select_first,
+                                decimals, u_applied, best_index, best_cost, static_cast<hipStream_t>(stream_ptr)));
     return MPCD_OK;
 }
 

@@ -152,9 +152,13 @@ __global__ void unnormalize_kernel(const float *x, int64_t n, int dim, const int
     }
 }
 
+// x0_dev == nullptr: every candidate starts from S.x0; else candidate b starts from x0_dev[b / group]
+// (closed loop: one plant state per group of candidates). flags[b / group] is that group's clip flag
+// (group = batch for the single-state case: one global flag).
 template <int SYS>
-__global__ __launch_bounds__(RT_THREADS) void rollout_cost_kernel(const SysK S, const float *u_norm, const int *flag,
-                                                                  int64_t batch, int H, double *cost)
+__global__ __launch_bounds__(RT_THREADS) void rollout_cost_kernel(const SysK S, const float *u_norm, const int *flags,
+                                                                  const double *x0_dev, int64_t group, int64_t batch,
+                                                                  int H, double *cost)
 {
     constexpr int nx = SysDim<SYS>::NX, nu = SysDim<SYS>::NU;
     extern __shared__ float su[];  // [RT_THREADS][H*nu + 1]
@@ -169,14 +173,14 @@ __global__ __launch_bounds__(RT_THREADS) void rollout_cost_kernel(const SysK S, 
     __syncthreads();
     const int64_t b = c0 + threadIdx.x;
     if (b >= batch) return;
-    const bool clip = *flag != 0;
+    const bool clip = flags[b / group] != 0;
     float mn[nu], mx[nu];
 #pragma unroll
     for (int i = 0; i < nu; ++i) { mn[i] = S.umin[i]; mx[i] = S.umax[i]; }
     const float *ur = su + threadIdx.x * stride;
     double x[nx], xn[nx], u[nu];
 #pragma unroll
-    for (int i = 0; i < nx; ++i) x[i] = S.x0[i];
+    for (int i = 0; i < nx; ++i) x[i] = x0_dev ? x0_dev[(b / group) * nx + i] : S.x0[i];
     double J;
     if (S.cost_kind == MPCD_COST_CALMPC) {
         // calMPCCost (Cart_Diffusion_inference.py:247-283); num_u = 1 (batch axis of u_hor)
@@ -208,6 +212,103 @@ __global__ __launch_bounds__(RT_THREADS) void rollout_cost_kernel(const SysK S, 
         }
     }
     cost[b] = J;
+}
+
+// Per-group clip flags: flags[g] = any element of x[g*group_elems, (g+1)*group_elems) outside
+// [-1-1e-4, 1+1e-4] (LimitsNormalizer's rule applied to each plant state's own candidate batch).
+__global__ void clip_flags_kernel(const float *x, int64_t n, int64_t group_elems, int *flags)
+{
+    const float hi = (float)(1.0 + 1e-4), lo = (float)(-1.0 - 1e-4);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float v = x[i];
+        if ((v > hi) | (v < lo)) atomicOr(flags + i / group_elems, 1);
+    }
+}
+
+// normalize_condition for a batch of plant states (normalization.py:149-154 in fp64, then the net's
+// .float()): ctx[m][c] = fp32(2 * ((x[m][c] - min[c]) / den[c]) - 1), den = fp32(max - min).
+struct NormK {
+    double mn[16], den[16];
+};
+__global__ void normalize_states_kernel(const double *x, int64_t M, int C, const NormK nk, float *out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M * C) return;
+    const int c = (int)(i % C);
+    out[i] = (float)(2.0 * ((x[i] - nk.mn[c]) / nk.den[c]) - 1.0);
+}
+
+// One closed-loop control step per plant state m (one workgroup each): the candidate of its group
+// [m*group, (m+1)*group) with the lowest cost (NaN = +inf, lowest index on ties; or the group's first
+// candidate, the reference scripts' n_samples = 1 convention), its u[0] unnormalised with the
+// group's clip flag and rounded to `decimals` places (the reference's round(u, 4) on the fp32 value
+// promoted to double; < 0: none), then the plant step x[m] <- f(x[m], u0) in fp64.
+constexpr int CS_THREADS = 256;
+template <int SYS>
+__global__ __launch_bounds__(CS_THREADS) void control_step_kernel(const SysK S, double *x_dev, int64_t group,
+                                                                  const float *u_norm, int H, const double *cost,
+                                                                  const int *flags, int select_first, int decimals,
+                                                                  double *u_applied, int64_t *best_idx, double *best_cost)
+{
+    constexpr int nx = SysDim<SYS>::NX, nu = SysDim<SYS>::NU;
+    __shared__ double sv[CS_THREADS];
+    __shared__ int64_t si[CS_THREADS];
+    const int64_t m = blockIdx.x, base = m * group;
+    double bv = INFINITY;
+    int64_t bi = -1;
+    if (select_first) {
+        if (threadIdx.x == 0) {
+            bi = base;
+            bv = cost[base];
+        }
+    } else {
+        for (int64_t i = threadIdx.x; i < group; i += CS_THREADS) {
+            double v = cost[base + i];
+            if (isnan(v)) v = INFINITY;
+            if (bi < 0 || v < bv) {
+                bv = v;
+                bi = base + i;
+            }
+        }
+    }
+    sv[threadIdx.x] = bv;
+    si[threadIdx.x] = bi;
+    __syncthreads();
+    for (int w = CS_THREADS / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+            const double ov = sv[threadIdx.x + w];
+            const int64_t oi = si[threadIdx.x + w];
+            const double mv = sv[threadIdx.x];
+            const int64_t mi = si[threadIdx.x];
+            if (oi >= 0 && (mi < 0 || ov < mv || (ov == mv && oi < mi))) {
+                sv[threadIdx.x] = ov;
+                si[threadIdx.x] = oi;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    const int64_t idx = si[0];
+    const bool clip = flags[m] != 0;
+    double x[nx], xn[nx], u[nu];
+#pragma unroll
+    for (int i = 0; i < nx; ++i) x[i] = x_dev[m * nx + i];
+#pragma unroll
+    for (int i = 0; i < nu; ++i) {
+        double v = (double)unnorm1(u_norm[(size_t)idx * H * nu + i], clip, S.umin[i], S.umax[i]);
+        if (decimals >= 0) {
+            const double sc = pow(10.0, (double)decimals);
+            v = rint(v * sc) / sc;
+        }
+        u[i] = v;
+    }
+    dyn_step<SYS>(S, x, u, xn);
+#pragma unroll
+    for (int i = 0; i < nx; ++i) x_dev[m * nx + i] = xn[i];
+#pragma unroll
+    for (int i = 0; i < nu; ++i) u_applied[m * nu + i] = u[i];
+    best_idx[m] = idx;
+    best_cost[m] = cost[idx];
 }
 
 // Single-workgroup argmin: NaN -> +inf; ties -> lowest index.
@@ -267,10 +368,11 @@ hipError_t launch_unnormalize(const float *x, int64_t n, int dim, const int *fla
     return hipGetLastError();
 }
 
-hipError_t launch_rollout_cost(const mpcd_system_desc &d, const double *x0_host, const float *u_norm,
-                               const float *umin_host, const float *umax_host, const int *flag_dev, int64_t batch, int H,
-                               double *cost, hipStream_t stream)
+hipError_t launch_rollout_cost(const mpcd_system_desc &d, const double *x0_host, const double *x0_dev, int64_t group,
+                               const float *u_norm, const float *umin_host, const float *umax_host, const int *flag_dev,
+                               int64_t batch, int H, double *cost, hipStream_t stream)
 {
+    if (group < 1) group = batch;
     SysK S = {};
     S.system = d.system;
     S.cost_kind = d.cost_kind;
@@ -279,15 +381,15 @@ hipError_t launch_rollout_cost(const mpcd_system_desc &d, const double *x0_host,
     for (int i = 0; i < 24; ++i) S.params[i] = d.params[i];
     for (int i = 0; i < 12; ++i) { S.Q[i] = d.Q[i]; S.P[i] = d.P[i]; S.xr[i] = d.x_ref[i]; }
     for (int i = 0; i < 4; ++i) S.R[i] = d.R[i];
-    for (int i = 0; i < d.n_x; ++i) S.x0[i] = x0_host[i];
+    for (int i = 0; i < d.n_x; ++i) S.x0[i] = x0_host ? x0_host[i] : 0.0;
     for (int i = 0; i < d.n_u; ++i) { S.umin[i] = umin_host[i]; S.umax[i] = umax_host[i]; }
     const size_t lds = sizeof(float) * RT_THREADS * (H * d.n_u + 1);
     const dim3 grid((unsigned)((batch + RT_THREADS - 1) / RT_THREADS));
 #define MPCD_ROLLOUT(SYS_)                                                                                          \
     case SYS_:                                                                                                      \
         if (d.n_x != SysDim<SYS_>::NX || d.n_u != SysDim<SYS_>::NU) return hipErrorInvalidValue;                    \
-        hipLaunchKernelGGL(rollout_cost_kernel<SYS_>, grid, dim3(RT_THREADS), lds, stream, S, u_norm, flag_dev, batch, H, \
-                           cost);                                                                                   \
+        hipLaunchKernelGGL(rollout_cost_kernel<SYS_>, grid, dim3(RT_THREADS), lds, stream, S, u_norm, flag_dev, x0_dev, \
+                           group, batch, H, cost);                                                                  \
         break;
     switch (d.system) {
         MPCD_ROLLOUT(MPCD_SYS_CARTPOLE_LIN5)
@@ -305,5 +407,63 @@ hipError_t launch_rollout_cost(const mpcd_system_desc &d, const double *x0_host,
 hipError_t launch_argmin(const double *cost, int64_t n, int64_t offset, mpcd_best *best, hipStream_t stream)
 {
     hipLaunchKernelGGL(argmin_kernel, dim3(1), dim3(1024), 0, stream, cost, n, offset, best);
+    return hipGetLastError();
+}
+
+hipError_t launch_clip_flags(const float *x, int64_t n_groups, int64_t group_elems, int *flags_dev, hipStream_t stream)
+{
+    hipError_t e = hipMemsetAsync(flags_dev, 0, sizeof(int) * n_groups, stream);
+    if (e != hipSuccess) return e;
+    const int64_t n = n_groups * group_elems;
+    const int64_t blocks = std::min<int64_t>(4096, (n + 255) / 256);
+    hipLaunchKernelGGL(clip_flags_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, stream, x, n,
+                       group_elems, flags_dev);
+    return hipGetLastError();
+}
+
+hipError_t launch_normalize_states(const double *x, int64_t M, int C, const float *mn_host, const float *mx_host,
+                                   float *out, hipStream_t stream)
+{
+    NormK nk;
+    for (int i = 0; i < 16; ++i) {
+        nk.mn[i] = i < C ? (double)mn_host[i] : 0.0;
+        nk.den[i] = i < C ? (double)(mx_host[i] - mn_host[i]) : 1.0;  // fp32 subtraction, then promoted
+    }
+    const int64_t n = M * C;
+    hipLaunchKernelGGL(normalize_states_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, x, M, C, nk, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_control_step(const mpcd_system_desc &d, double *x_dev, int64_t M, int64_t group, const float *u_norm,
+                               int H, const double *cost, const float *umin_host, const float *umax_host,
+                               const int *flags_dev, int select_first, int decimals, double *u_applied,
+                               int64_t *best_idx, double *best_cost, hipStream_t stream)
+{
+    SysK S = {};
+    S.system = d.system;
+    S.cost_kind = d.cost_kind;
+    S.nx = d.n_x;
+    S.nu = d.n_u;
+    for (int i = 0; i < 24; ++i) S.params[i] = d.params[i];
+    for (int i = 0; i < d.n_u; ++i) {
+        S.umin[i] = umin_host[i];
+        S.umax[i] = umax_host[i];
+    }
+#define MPCD_CSTEP(SYS_)                                                                                         \
+    case SYS_:                                                                                                   \
+        if (d.n_x != SysDim<SYS_>::NX || d.n_u != SysDim<SYS_>::NU) return hipErrorInvalidValue;                 \
+        hipLaunchKernelGGL(control_step_kernel<SYS_>, dim3((unsigned)M), dim3(CS_THREADS), 0, stream, S, x_dev, group, \
+                           u_norm, H, cost, flags_dev, select_first, decimals, u_applied, best_idx, best_cost);  \
+        break;
+    switch (d.system) {
+        MPCD_CSTEP(MPCD_SYS_CARTPOLE_LIN5)
+        MPCD_CSTEP(MPCD_SYS_CARTPOLE_NL5)
+        MPCD_CSTEP(MPCD_SYS_CARTPOLE_ZOH4)
+        MPCD_CSTEP(MPCD_SYS_DOUBLE_INT2D)
+        MPCD_CSTEP(MPCD_SYS_PENDULUM)
+        MPCD_CSTEP(MPCD_SYS_QUADROTOR12)
+    default: return hipErrorInvalidValue;
+    }
+#undef MPCD_CSTEP
     return hipGetLastError();
 }

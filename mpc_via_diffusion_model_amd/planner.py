@@ -71,6 +71,14 @@ class MPCResult:
     u_norm: torch.Tensor    # [B_local, H, d] this rank's normalised samples
 
 
+@dataclass
+class ClosedLoopResult:
+    x: np.ndarray           # [M, T+1, n_x] plant states (fp64), x[:, 0] = the initial states
+    u: np.ndarray           # [M, T, n_u] applied actions (unnormalised, rounded as requested)
+    cost: np.ndarray        # [M, T] cost of the selected candidate at each step
+    index: np.ndarray       # [M, T] global index of the selected candidate in that step's batch
+
+
 class DiffusionMPC:
     def __init__(self, spec, params, tables=None, variance_schedule="exponential", n_diffusion_steps=100,
                  device=None, context_limits=None, action_limits=None):
@@ -294,6 +302,58 @@ class DiffusionMPC:
                                       ctypes.c_void_p(self._best.data_ptr()), self._stream()), "mpcd_argmin")
         host = self._best.cpu()
         return int(host.view(torch.int64)[1]), float(host[0])
+
+    def closed_loop(self, x0_states, system: System, iterations, n_samples=1, w=0.01, sample_fn="ddpm_cfg",
+                    n_wo_noise=0, ddim_steps=None, clamp_x0=False, select="argmin", decimals=4, seed=0, noise=None):
+        """Closed-loop diffusion MPC for M plant states at once, resident on the device.
+        The reference runs one initial state at a time on the host (Cart_Diffusion_inference.py:405-512:
+        normalize_condition -> run_CFG -> unnormalize -> u0 = round(u[0], 4) -> x = f(x, u0), repeated
+        ITERATIONS times per initial state). Here every iteration is: per-state contexts
+        (mpcd_normalize_states), n_samples candidates per state in one sampler launch, per-state clip flags,
+        rollout + cost from each state's own x, and mpcd_control_step (per-state selection, u0, plant step);
+        nothing returns to the host until the end. select: "argmin" (lowest cost) or "first" (candidate 0 of
+        each group: the reference scripts with n_samples = 1). Per-state contexts use the exact-f32 MLP
+        kernel (the split-bf16 one needs a shared context). noise: optional callable it -> injected sampler
+        noise [S+1, M*n_samples, H, d] (parity tests); default in-kernel Philox keyed by (seed + it)."""
+        if select not in ("argmin", "first"):
+            raise ValueError("select must be 'argmin' or 'first'")
+        x0 = np.ascontiguousarray(np.atleast_2d(np.asarray(x0_states, dtype=np.float64)))
+        M, nx = x0.shape
+        if nx != system.n_x or system.n_u != self.spec.state_dim:
+            raise ValueError(f"system {system.name}: n_x={system.n_x}, n_u={system.n_u}; states have {nx} columns, "
+                             f"the net samples {self.spec.state_dim} actions")
+        if self.spec.context_dim != nx:
+            raise ValueError(f"closed loop conditions on the plant state: context_dim {self.spec.context_dim} != n_x {nx}")
+        T, n, H, d = int(iterations), int(n_samples), self.spec.horizon, self.spec.state_dim
+        B, dev, st = M * n, self.device, self._stream()
+        desc = system.desc()
+        x = torch.from_numpy(x0).to(dev)
+        xs = torch.empty((T + 1, M, nx), dtype=torch.float64, device=dev)
+        us = torch.empty((T, M, d), dtype=torch.float64, device=dev)
+        cs = torch.empty((T, M), dtype=torch.float64, device=dev)
+        ix = torch.empty((T, M), dtype=torch.int64, device=dev)
+        ctx = torch.empty((M, nx), dtype=torch.float32, device=dev)
+        flags = torch.empty(M, dtype=torch.int32, device=dev)
+        cost = torch.empty(B, dtype=torch.float64, device=dev)
+        u_norm = torch.empty((B, H, d), dtype=torch.float32, device=dev)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        xs[0] = x
+        for it in range(T):
+            N.check(self._lib.mpcd_normalize_states(self._ctx, ptr(x), M, nx, self.ctx_min.ctypes.data,
+                                                    self.ctx_max.ctypes.data, ptr(ctx), st), "mpcd_normalize_states")
+            self.sample_trajectories(ctx.repeat_interleave(n, dim=0), B, H, w, sample_fn, n_wo_noise, ddim_steps,
+                                     clamp_x0, seed + it, 0, None if noise is None else noise(it), False, out=u_norm)
+            N.check(self._lib.mpcd_clip_flags(self._ctx, ptr(u_norm), M, n * H * d, ptr(flags), st), "mpcd_clip_flags")
+            N.check(self._lib.mpcd_rollout_cost_grouped(self._ctx, ctypes.byref(desc), ptr(x), n, ptr(u_norm),
+                                                        self.act_min.ctypes.data, self.act_max.ctypes.data, B, H,
+                                                        ptr(flags), ptr(cost), st), "mpcd_rollout_cost_grouped")
+            N.check(self._lib.mpcd_control_step(self._ctx, ctypes.byref(desc), ptr(x), M, n, ptr(u_norm), H, ptr(cost),
+                                                self.act_min.ctypes.data, self.act_max.ctypes.data, ptr(flags),
+                                                1 if select == "first" else 0, -1 if decimals is None else int(decimals),
+                                                ptr(us[it]), ptr(ix[it]), ptr(cs[it]), st), "mpcd_control_step")
+            xs[it + 1] = x
+        return ClosedLoopResult(x=xs.transpose(0, 1).cpu().numpy(), u=us.transpose(0, 1).cpu().numpy(),
+                                cost=cs.t().cpu().numpy(), index=ix.t().cpu().numpy())
 
     def mpc_step(self, x0, system: System, n_samples, w=0.01, sample_fn="ddpm_cfg", n_wo_noise=0, ddim_steps=None,
                  clamp_x0=False, seed=0, noise=None, group=None):

@@ -1,0 +1,86 @@
+"""On-disk formats: trained-model args.yaml + state_dict -> NetSpec inference,
+training-tensor and inference-dump layouts. CPU only."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import yaml
+
+from mpc_via_diffusion_model_amd import formats as F
+from oracle import nets
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ARGS = os.path.join(HERE, "golden", "cart_pole_84000_test1_args.yaml")
+KAT3 = os.path.join(HERE, "golden", "cart_pole_84000_test1_ema.safetensors")
+
+
+def _trained_dir(tmp_path):
+    """A trained-model directory in the reference layout, from the committed fixtures."""
+    from safetensors.torch import load_file
+    d = tmp_path / "final"
+    (d / "checkpoints").mkdir(parents=True)
+    (d / "args.yaml").write_text(open(ARGS).read())
+    torch.save(load_file(KAT3), d / "checkpoints" / "ema_model_current_state_dict.pth")
+    return str(d)
+
+
+def test_args_yaml_fields():
+    a = yaml.safe_load(open(ARGS))
+    assert a["n_diffusion_steps"] == 25 and a["variance_schedule"] == "exponential"
+    assert a["unet_dim_mults_option"] == 0 and a["unet_input_dim"] == 32 and a["use_ema"] is True
+
+
+def test_infer_spec_trained_cartpole(tmp_path):
+    d = _trained_dir(tmp_path)
+    args = F.read_args(d)
+    sd = F.load_state_dict(F.checkpoint_path(d, args=args))
+    spec = F.infer_spec(sd, args)
+    assert (spec.kind, spec.state_dim, spec.context_dim, spec.horizon, spec.base_dim, tuple(spec.dim_mults)) == \
+        ("unet", 1, 5, 32, 32, (1, 2, 4))
+    with pytest.raises(ValueError):
+        F.infer_spec(sd, dict(args, unet_dim_mults_option=1))
+
+
+def test_infer_spec_mlp_and_unet_shapes():
+    sd = {"model." + k: v for k, v in nets.ConditionedMLPNet(state_dim=2, horizon=32, context_dim=4).state_dict().items()}
+    spec = F.infer_spec(sd, {}, horizon=32)
+    assert (spec.kind, spec.state_dim, spec.context_dim, spec.horizon) == ("mlp", 2, 4, 32)
+    sd = nets.ConditionedTemporalUnet(state_dim=7, context_dim=20).state_dict()
+    spec = F.infer_spec(sd, {"unet_dim_mults_option": 0}, horizon=128)
+    assert (spec.kind, spec.state_dim, spec.context_dim, spec.horizon) == ("unet", 7, 20, 128)
+    with pytest.raises(ValueError):
+        F.infer_spec(sd, {"dataset_subdir": "Unknown"})
+
+
+def test_state_dict_loader_is_weights_only(tmp_path):
+    p = tmp_path / "x.pth"
+    torch.save({"a": torch.ones(2)}, p)
+    assert torch.equal(F.load_state_dict(str(p))["a"], torch.ones(2))
+    torch.save({"a": [1, 2]}, p)
+    with pytest.raises(ValueError):
+        F.load_state_dict(str(p))
+
+
+def test_training_tensor_round_trip(tmp_path):
+    u, x0, j = torch.randn(10, 32, 1), torch.randn(10, 5, dtype=torch.float64), torch.rand(10)
+    paths = F.save_training_tensors(str(tmp_path), u, x0, j, prefix="grp_0_")
+    assert os.path.basename(paths["u"]) == "grp_0_u_tensor_10-32-1.pt"
+    assert torch.equal(F.load_training_tensor(paths["u"]), u)
+    assert torch.equal(F.load_training_tensor(paths["x0"]), x0)
+    assert torch.equal(F.load_training_tensor(paths["J"]), j)
+    with pytest.raises(ValueError):
+        F.save_training_tensors(str(tmp_path), u[:, :, 0], x0)
+
+
+def test_inference_dump_layout(tmp_path):
+    T, H = 6, 32
+    u = np.random.default_rng(0).normal(size=(T, 1))
+    uh = np.random.default_rng(1).normal(size=(T, H, 1))
+    xh = np.random.default_rng(2).normal(size=(T, H + 1, 5))
+    names = F.save_inference_results(str(tmp_path), u, uh, xh)
+    assert names == ["u_diffusion.npy", "u_horizon_diffusion.npy", "x_diffusion_horizon.npy"]
+    r = F.load_inference_results(str(tmp_path))
+    assert r["u_diffusion"].shape == (1, T) and r["u_horizon_diffusion"].shape == (T, H)
+    assert r["x_diffusion_horizon"].shape == (T, H + 1, 5)
+    np.testing.assert_array_equal(r["u_diffusion"][0], np.round(u[:, 0], 4))

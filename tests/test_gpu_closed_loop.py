@@ -1,0 +1,78 @@
+"""GPU: closed-loop diffusion MPC over many plant states at once against an oracle
+restatement of the reference loop (Cart_Diffusion_inference.py:405-512) run per state on the CPU."""
+import numpy as np
+import pytest
+import torch
+
+from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec, systems
+from oracle import normalizer as onorm
+from oracle import sampler as osam
+from oracle import schedule as osch
+from oracle import systems as osys
+
+from ._util import make_mlp
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_closed_loop(net, bufs, x0, sysname, T, n, H, d, w, noise, cmin, cmax, amin, amax, select):
+    x = np.array(x0, dtype=np.float64)
+    M = x.shape[0]
+    xs, us, idx = [x.copy()], [], []
+    for it in range(T):
+        ctx = onorm.normalize(torch.from_numpy(x), torch.from_numpy(cmin), torch.from_numpy(cmax)).float()
+        un = osam.ddpm_cfg(net, bufs, ctx.repeat_interleave(n, 0), w, M * n, H, noise=noise(it))
+        u_it, i_it = [], []
+        for m in range(M):
+            g = un[m * n:(m + 1) * n]
+            u = onorm.unnormalize(g, torch.from_numpy(amin), torch.from_numpy(amax))
+            cost = osys.rollout_cost(sysname, x[m], u.double().numpy())
+            i = 0 if select == "first" else int(osys.argmin(cost))
+            u0 = np.array([round(float(v), 4) for v in u[i, 0]], dtype=np.float64)
+            x[m] = osys.step(sysname, x[m], u0)
+            u_it.append(u0)
+            i_it.append(m * n + i)
+        xs.append(x.copy())
+        us.append(np.stack(u_it))
+        idx.append(i_it)
+    return np.stack(xs, 1), np.stack(us, 1), np.array(idx).T
+
+
+@pytest.mark.parametrize("select", ["argmin", "first"])
+def test_closed_loop_matches_oracle(select):
+    M, n, T, H, d, C, N = 5, 16, 4, 16, 2, 4, 25
+    net = make_mlp(d, H, C, seed=31)
+    plan = DiffusionMPC(NetSpec("mlp", d, H, C), net.state_dict(), variance_schedule="exponential", n_diffusion_steps=N,
+                        context_limits=(-2 * np.ones(C), 2 * np.ones(C)), action_limits=(-np.ones(d), np.ones(d)))
+    sysm = systems.get("double_int2d")
+    x0 = np.random.default_rng(3).uniform(-1.5, 1.5, (M, 4))
+    g = torch.Generator().manual_seed(17)
+    noises = [torch.randn(N + 1, M * n, H, d, generator=g) for _ in range(T)]
+    res = plan.closed_loop(x0, sysm, T, n_samples=n, w=0.01, select=select, noise=lambda it: noises[it])
+    xr, ur, ir = _oracle_closed_loop(net, osch.buffers("exponential", N), x0, "double_int2d", T, n, H, d, 0.01,
+                                     lambda it: noises[it], -2 * np.ones(C, np.float32), 2 * np.ones(C, np.float32),
+                                     -np.ones(d, np.float32), np.ones(d, np.float32), select)
+    assert res.x.shape == (M, T + 1, 4) and res.u.shape == (M, T, d) and res.index.shape == (M, T)
+    np.testing.assert_array_equal(res.index, ir)
+    # u0 is rounded to 4 decimals: a sampler difference within the 1e-4 parity bar can move it by 1e-4
+    assert np.abs(res.u - ur).max() <= 1.01e-4
+    assert np.abs(res.x - xr).max() <= 1e-4 * max(1.0, np.abs(xr).max())
+
+
+def test_closed_loop_many_states_philox():
+    """A 5x5 grid of initial states (Cart_Diffusion_inference.py:29-30 style), 20 iterations, 64
+    candidates each: finite, deterministic, selections inside each state's own group."""
+    M, n, T, H, d, C, N = 25, 64, 20, 16, 2, 4, 25
+    net = make_mlp(d, H, C, seed=2)
+    plan = DiffusionMPC(NetSpec("mlp", d, H, C), net.state_dict(), variance_schedule="exponential", n_diffusion_steps=N,
+                        context_limits=(-2 * np.ones(C), 2 * np.ones(C)))
+    sysm = systems.get("double_int2d")
+    gx, gy = np.meshgrid(np.linspace(-1, 1, 5), np.linspace(-1, 1, 5))
+    x0 = np.stack([gx.ravel(), gy.ravel(), np.zeros(M), np.zeros(M)], 1)
+    a = plan.closed_loop(x0, sysm, T, n_samples=n, seed=5)
+    b = plan.closed_loop(x0, sysm, T, n_samples=n, seed=5)
+    assert np.isfinite(a.x).all() and np.isfinite(a.cost).all()
+    np.testing.assert_array_equal(a.x, b.x)
+    assert (np.abs(a.u) <= 1.0 + 1e-12).all()
+    # rows of the selected candidates stay inside each state's group
+    assert ((a.index // n) == np.arange(M)[:, None]).all()

@@ -131,3 +131,24 @@ def test_unet_philox_shard_invariance():
     b = plan.sample_trajectories(ctx, B - 16, H, seed=5, global_offset=16)
     assert torch.equal(full, torch.cat([a, b]))
     assert torch.isfinite(full).all() and float(full.abs().max()) <= 1.0 + 1e-6
+
+
+def test_kat3_through_trained_model_loader(tmp_path):
+    """the reference trained-model directory layout (args.yaml + weights-only
+    ema_model_current_state_dict.pth) through formats.load_trained, then KAT3 on the GPU."""
+    from safetensors.torch import load_file
+    from mpc_via_diffusion_model_amd import formats
+    d = tmp_path / "final"
+    (d / "checkpoints").mkdir(parents=True)
+    (d / "args.yaml").write_text(open(os.path.join(HERE, "golden", "cart_pole_84000_test1_args.yaml")).read())
+    torch.save(load_file(os.path.join(HERE, "golden", "cart_pole_84000_test1_ema.safetensors")),
+               d / "checkpoints" / "ema_model_current_state_dict.pth")
+    plan = formats.load_trained(str(d))
+    assert (plan.spec.kind, plan.spec.state_dim, plan.spec.context_dim, plan.spec.horizon) == ("unet", 1, 5, 32)
+    torch.manual_seed(0)
+    ctx = torch.rand(1, 5) * 2 - 1
+    noise = torch.stack([torch.randn(1, 32, 1) for _ in range(31)])
+    chain = plan.run_CFG(ctx, None, 0.01, n_samples=1, horizon=32, return_chain=True, noise=noise,
+                         n_diffusion_steps_without_noise=5)
+    np.testing.assert_allclose(chain[-1, 0, :8, 0].cpu().numpy(),
+                               [0.9998, 0.9592, 0.9130, 0.8686, 0.8263, 0.7862, 0.7497, 0.7155], atol=5e-5)
