@@ -17,17 +17,17 @@ MPCD_DEV f32x4 ldg4(const float *p) { return *reinterpret_cast<const f32x4 __att
 // __syncthreads() fence may add (register-destination global prefetches stay in flight).
 MPCD_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// Mish(x) = x * tanh(softplus(x)) (torch.nn.Mish). With n = e^x,
-// tanh(log1p(n)) = n(n+2) / (n(n+2) + 2): one v_exp_f32 and one v_rcp_f32 (1 ulp each) plus 7 plain
-// VALU ops that the compiler packs in pairs (v_pk_*). Clamping x at 40 before the exp keeps n(n+2)
-// finite, and for x > 20 the fp32 factor is exactly 1, so no compare/select is needed (huge x pass
-// through unchanged as in torch). Max relative
-// error vs float64 Mish 6.7e-7 over [-30, 60] (x*log2(e) is rounded before the exp).
+// Mish(x) = x * tanh(softplus(x)) (torch.nn.Mish). With n = e^x, tanh(log1p(n)) = 1 - 2 / (n(n+2) + 2):
+// one v_exp_f32 and one v_rcp_f32 (1 ulp each) plus a multiply, an add, two FMAs and the final product
+// (the f32 MFMA and the VALU share issue on gfx950, so every epilogue op counts). Overflow is benign:
+// x -> +inf gives n(n+2)+2 = inf, factor 1, Mish(x) = x as in torch; no clamp or select needed.
+// Error vs float64 Mish over [-30, 60]: <= 1e-6 absolute everywhere (the 1 - 2r cancellation costs
+// relative accuracy only where Mish(x) is ~0, x < -5), 7e-7 relative for |Mish| > 1e-2.
 MPCD_DEV float mish(float x)
 {
-    const float n = __builtin_amdgcn_exp2f(fminf(x, 40.0f) * 1.44269504088896341f);
-    const float p = n * (n + 2.0f);
-    return x * (p * __builtin_amdgcn_rcpf(p + 2.0f));  // factor <= 1: no overflow for huge x
+    const float n = __builtin_amdgcn_exp2f(x * 1.44269504088896341f);
+    const float r = __builtin_amdgcn_rcpf(__builtin_fmaf(n, n + 2.0f, 2.0f));
+    return x * __builtin_fmaf(-2.0f, r, 1.0f);
 }
 
 // The accurate reference form (expf + IEEE divide), kept for the low-volume prologue kernels.
