@@ -29,8 +29,15 @@ def test_oracle_reproduces_golden(name, tmp_path, monkeypatch):
     monkeypatch.setattr(G, "HERE", str(tmp_path))
     G.make(name, c)
     new = dict(np.load(os.path.join(tmp_path, name + ".npz")))
-    for k in ("noise", "context", "x0", "chain", "cost", "best"):
+    # inputs are bit-exact (seeded torch RNG); outputs go through torch-CPU GEMMs, whose summation order
+    # depends on the host ISA / thread count (fixtures made on another CPU differ by ~1 ulp)
+    for k in ("noise", "context", "x0"):
         np.testing.assert_array_equal(new[k], fx[k], err_msg=k)
+    assert_traj_close(torch.from_numpy(new["chain"]), torch.from_numpy(fx["chain"]), rel=1e-5, abs_elem=1e-5,
+                      what=name)
+    np.testing.assert_allclose(new["cost"], fx["cost"], rtol=1e-4)
+    b, i = int(new["best"]), int(fx["best"])
+    assert b == i or abs(fx["cost"][b] - fx["cost"][i]) <= 1e-4 * abs(fx["cost"][i])
 
 
 @pytest.mark.gpu
