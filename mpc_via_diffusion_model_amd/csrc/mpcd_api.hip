@@ -178,9 +178,8 @@ int check_desc(const mpcd_net_desc *d)
         return fail(MPCD_EINVAL, "bad net dims");
     for (int i = 0; i < d->n_mults; ++i)
         if (d->mults[i] < 1) return fail(MPCD_EINVAL, "bad dim_mults");
-    if (d->dtype == MPCD_F16) return fail(MPCD_EUNSUP, "fp16 hidden activations are not built");
-    if (d->dtype == MPCD_F32X3 && d->kind != MPCD_NET_MLP) return fail(MPCD_EUNSUP, "MPCD_F32X3 is MLP-only");
-    if (d->dtype != MPCD_F32 && d->dtype != MPCD_F32X3) return fail(MPCD_EINVAL, "bad dtype %d", d->dtype);
+    if (d->dtype == MPCD_F16 && d->kind != MPCD_NET_UNET) return fail(MPCD_EUNSUP, "MPCD_F16 is UNet-only");
+    if (d->dtype != MPCD_F32 && d->dtype != MPCD_F32X3 && d->dtype != MPCD_F16) return fail(MPCD_EINVAL, "bad dtype %d", d->dtype);
     return MPCD_OK;
 }
 

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <functional>
+#include <string>
 #include <vector>
 
 #include "../../include/mpcd.h"
@@ -21,11 +22,40 @@ struct ConvLayer {
     const float *gn_w, *gn_b;  // GroupNorm affine or null
     int groups;
     int cond_off;      // column of this block in tproj/cproj, -1 = none
+    // bf16 / f16 MFMA form (MPCD_F32X3, MPCD_F16; unet_mx.hip): [parities][coutp/16][kc][planes][64][8]
+    const uint16_t *wmx;
+    int cinp8;         // cin padded to 8 / 16 / a multiple of 32 (K per tap)
+    int kc;            // k-chunks of 32 per parity
+};
+
+// One fused conv launch of the bf16/f16-MFMA family (unet_mx.hip).
+struct ConvMK {
+    const float *xa, *xb;   // inputs [x_rows][lin][ca], [x_rows][lin][cb] (channel concat)
+    int ca, cb, cinp, kc;   // channels, padded channels per tap, k-chunks of 32
+    int64_t x_rows;         // row r reads input row r % x_rows
+    const uint16_t *w;      // packed A fragments
+    const float *bias;
+    const float *gn_w, *gn_b;
+    int groups;
+    const float *tp, *cp;   // cond (EPI_GN_MISH_COND): tproj row + cond_off, cproj + cond_off or null
+    int64_t cp_stride, b_cand;
+    const float *res;       // residual [rows][lout][cout] (EPI_GN_MISH_RES)
+    float *out;             // [rows][lout][cout]
+    int64_t rows;
+    int lin, lout, cout, coutp;
+    int rb;                 // rows per workgroup
+    int halo_l, halo_r;     // staged input window = [-halo_l, lin + halo_r)
+    int cs;                 // staged bytes per position (one plane)
+    int epi;                // EPI_*
+    int alias;              // 1: the fp32 output tile reuses the staged-input LDS
+    int stat_off;           // LDS byte offset of the GroupNorm statistics (then the per-channel table)
+    int cpg_shift;          // log2(cout / groups)
 };
 
 struct UnetWeights {
     bool ready = false;
     int n_layers = 0;
+    int planes = 0;                 // 0: fp32 MFMA kernels (unet.hip); 3: split-bf16, 1: f16 (unet_mx.hip)
     std::vector<ConvLayer> layers;  // in execution order (see unet.hip build_plan)
 };
 
@@ -50,6 +80,17 @@ struct UnetSampleArgs {
     float *eps_cond, *eps_uncond;  // MODE_EPS / MODE_EPS1 outputs
     const float *x_in;             // MODE_EPS / MODE_EPS1 input
 };
+
+// epilogue kinds shared by both conv families
+enum { UCONV_SAME5 = 0, UCONV_DOWN3 = 1, UCONV_UP4 = 2, UCONV_PW1 = 3 };
+enum { UEPI_BIAS = 0, UEPI_GN_MISH = 1, UEPI_GN_MISH_COND = 2, UEPI_GN_MISH_RES = 3 };
+
+// Pack one conv for the MFMA-bf16/f16 kernels; planes = 3 (split-bf16, MPCD_F32X3) or 1 (f16, MPCD_F16).
+// w_host: conv [cout][cin][ks] or convT [cin][cout][4]. Appends to `pack` and sets L.wmx (offset), L.cinp8, L.kc.
+void unet_pack_mx(int kind, int cin, int cout, int planes, const float *w_host, ConvLayer &L,
+                  std::vector<uint16_t> &pack);
+// Choose rows per workgroup / tile shape and launch; kind = UCONV_*, planes 1 or 3.
+hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::string *why);
 
 using TensorLookup = std::function<const float *(const char *)>;
 

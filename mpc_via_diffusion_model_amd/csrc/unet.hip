@@ -395,7 +395,10 @@ int unet_prepare(const mpcd_net_desc &d, size_t, const TensorLookup &dev, const 
 {
     W.ready = false;
     W.layers.clear();
-    if (d.dtype != MPCD_F32) return uerr(MPCD_EUNSUP, "UNet: only fp32 hidden is built");
+    if (d.dtype != MPCD_F32 && d.dtype != MPCD_F32X3 && d.dtype != MPCD_F16)
+        return uerr(MPCD_EINVAL, "UNet: bad dtype");
+    const int planes = d.dtype == MPCD_F32X3 ? 3 : d.dtype == MPCD_F16 ? 1 : 0;  // 0: fp32 MFMA kernels
+    std::vector<uint16_t> packmx;
     if (d.horizon % (1 << (d.n_mults - 1)) != 0) return uerr(MPCD_EINVAL, "UNet: horizon must divide by 2^(levels-1)");
     const Dims m = dims_of(d);
     std::vector<float> pack;
@@ -436,6 +439,7 @@ int unet_prepare(const mpcd_net_desc &d, size_t, const TensorLookup &dev, const 
             return;
         }
         pack_conv(kind, cin, cout, wh, bd, L, pack);
+        if (planes) unet_pack_mx(kind, cin, cout, planes, wh, L, packmx);
         L.groups = gn ? group_norm_n_groups(cout) : 1;
         L.cond_off = cond;
         L.gn_w = L.gn_b = nullptr;
@@ -475,7 +479,9 @@ int unet_prepare(const mpcd_net_desc &d, size_t, const TensorLookup &dev, const 
     gn_of("final_conv.0.block.2");
     conv(CONV_PW1, "final_conv.1", m.base, m.d, false, -1);
     if (rc) return uerr(rc, g_unet_err);
-    const size_t bytes = pack.size() * sizeof(float);
+    if (planes) pack.clear();  // the mx kernels read only their own pack
+    const size_t fbytes = (pack.size() * sizeof(float) + 255) / 256 * 256;
+    const size_t bytes = fbytes + packmx.size() * sizeof(uint16_t);
     if (bytes > pack_bytes) {
         if (pack_dev) (void)hipFree(pack_dev);
         pack_dev = nullptr;
@@ -483,9 +489,18 @@ int unet_prepare(const mpcd_net_desc &d, size_t, const TensorLookup &dev, const 
         if (hipMalloc(&pack_dev, bytes) != hipSuccess) return uerr(MPCD_ENOMEM, "hipMalloc(unet pack)");
         pack_bytes = bytes;
     }
-    if (hipMemcpy(pack_dev, pack.data(), bytes, hipMemcpyHostToDevice) != hipSuccess)
+    if (!pack.empty() && hipMemcpy(pack_dev, pack.data(), pack.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
         return uerr(MPCD_EHIP, "hipMemcpy(unet pack)");
-    for (auto &L : W.layers) L.w = static_cast<const float *>(pack_dev) + reinterpret_cast<size_t>(L.w);
+    if (!packmx.empty() && hipMemcpy(static_cast<char *>(pack_dev) + fbytes, packmx.data(),
+                                     packmx.size() * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess)
+        return uerr(MPCD_EHIP, "hipMemcpy(unet mx pack)");
+    for (auto &L : W.layers) {
+        L.w = planes ? nullptr : static_cast<const float *>(pack_dev) + reinterpret_cast<size_t>(L.w);
+        L.wmx = planes ? reinterpret_cast<const uint16_t *>(static_cast<char *>(pack_dev) + fbytes) +
+                             reinterpret_cast<size_t>(L.wmx)
+                       : nullptr;
+    }
+    W.planes = planes;
     W.n_layers = (int)W.layers.size();
     W.ready = true;
     return MPCD_OK;
@@ -592,6 +607,39 @@ int run_conv(Ctx &c, int epi, const float *xa, int ca, const float *xb, int cb, 
 {
     const ConvLayer &L = c.W->layers[c.li++];
     if (L.cin != ca + cb) return uerr(MPCD_EINVAL, "UNet plan: channel mismatch");
+    if (c.W->planes) {
+        ConvMK k{};
+        k.xa = xa;
+        k.xb = xb;
+        k.ca = ca;
+        k.cb = cb;
+        k.cinp = L.cinp8;
+        k.kc = L.kc;
+        k.x_rows = x_rows;
+        k.w = L.wmx;
+        k.bias = L.bias;
+        k.gn_w = L.gn_w;
+        k.gn_b = L.gn_b;
+        k.groups = L.groups;
+        k.tp = L.cond_off >= 0 ? c.tp + L.cond_off : nullptr;
+        k.cp = (L.cond_off >= 0 && c.cp) ? c.cp + L.cond_off : nullptr;
+        k.cp_stride = c.cp_stride;
+        k.b_cand = c.b_cand;
+        k.res = res;
+        k.out = out;
+        k.rows = c.rows;
+        k.lin = lin;
+        k.lout = L.kind == CONV_DOWN3 ? lin / 2 : L.kind == CONV_UP4 ? lin * 2 : lin;
+        k.cout = L.cout;
+        k.coutp = L.coutp;
+        k.epi = epi;
+        if (epi == EPI_GN_MISH_COND && !k.tp) return uerr(MPCD_EINVAL, "UNet plan: missing cond");
+        if (L.cout % L.groups != 0) return uerr(MPCD_EUNSUP, "UNet: cout not divisible by groups");
+        std::string why;
+        hipError_t e = unet_launch_mx(L.kind, c.W->planes, k, c.st, &why);
+        if (e != hipSuccess) return uerr(MPCD_EHIP, "mx conv launch: " + (why.empty() ? hipGetErrorString(e) : why));
+        return MPCD_OK;
+    }
     ConvK k{};
     k.xa = xa;
     k.xb = xb;

@@ -1,0 +1,559 @@
+// U-Net convolutions on the bf16 / f16 matrix cores (MPCD_F32X3 and MPCD_F16 nets).
+//
+// Same fused op per launch as unet.hip's fp32 conv_kernel (one conv of ResidualTemporalBlock /
+// Conv1dBlock / Downsample1d / Upsample1d, layers.py:258-355, with its bias -> GroupNorm -> Mish ->
+// + cond / + residual epilogue), but the implicit GEMM runs on v_mfma_f32_16x16x32_{bf16,f16}:
+//
+//  * MPCD_F32X3 (P = 3 planes): every fp32 operand is split into three bf16 terms (x = x0 + x1 + x2,
+//    exact to ~2^-27 relative) and each dot product accumulates the six partial products whose weight
+//    is >= 2^-16 of the leading one in fp32 (as mlp_x3.hip): fp32-level GEMM error at the bf16 rate.
+//  * MPCD_F16 (P = 1): fp16 operands, fp32 accumulation - BASELINE cfg 5's "fp16 hidden with MFMA GEMM".
+//
+// A workgroup (4 waves) owns rb whole rows (row = one candidate of one CFG branch). It stages the
+// rows' input window in LDS already split into bf16 / f16 planes, channels-last
+// [plane][row][position][channel] with a per-position stride whose 16-B count is odd (the 16 lanes of a
+// ds_read_b128 quarter hit distinct banks). The output tile [cout] x [rb * lout columns] is cut into
+// jobs of NN 16-channel n-tiles x NC 16-column c-tiles; a wave keeps the NN x NC accumulators, reads
+// each weight fragment (A, packed per 32-k chunk, streamed from L2 by buffer loads, next chunk in
+// flight) once for NC column tiles and each input fragment (B, LDS) once for NN channel tiles. The
+// K order is k = tap * cinp + ci, so one lane's 8 k-values are 8 consecutive channels of one tap:
+// the B fragment is one 16-byte LDS read. Accumulators start from the bias; the fp32 tile then goes
+// through LDS (reusing the staged input when one job per wave suffices) for the GroupNorm statistics
+// (fp64, shifted) and the elementwise epilogue, stored coalesced channels-last.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+
+#include "unet.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int MT = 256;  // threads per workgroup
+
+MPCD_DEV uint32_t pk_bf16(float lo, float hi)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, bf16x2));
+}
+MPCD_DEV uint32_t pk_f16(float lo, float hi)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, f16x2));
+}
+MPCD_DEV float bf_lo(uint32_t p) { return __builtin_bit_cast(float, p << 16); }
+MPCD_DEV float bf_hi(uint32_t p) { return __builtin_bit_cast(float, p & 0xffff0000u); }
+
+// 8 consecutive fp32 -> P planes of 8 values (16 bytes each)
+template <int P>
+MPCD_DEV void split8(const f32x4 &lo, const f32x4 &hi, u32x4 (&o)[P])
+{
+    if constexpr (P == 1) {
+        o[0] = u32x4{pk_f16(lo.x, lo.y), pk_f16(lo.z, lo.w), pk_f16(hi.x, hi.y), pk_f16(hi.z, hi.w)};
+    } else {
+        const uint32_t a0 = pk_bf16(lo.x, lo.y), a1 = pk_bf16(lo.z, lo.w), a2 = pk_bf16(hi.x, hi.y),
+                       a3 = pk_bf16(hi.z, hi.w);
+        const f32x4 rl = lo - f32x4{bf_lo(a0), bf_hi(a0), bf_lo(a1), bf_hi(a1)};
+        const f32x4 rh = hi - f32x4{bf_lo(a2), bf_hi(a2), bf_lo(a3), bf_hi(a3)};
+        const uint32_t b0 = pk_bf16(rl.x, rl.y), b1 = pk_bf16(rl.z, rl.w), b2 = pk_bf16(rh.x, rh.y),
+                       b3 = pk_bf16(rh.z, rh.w);
+        const f32x4 sl = rl - f32x4{bf_lo(b0), bf_hi(b0), bf_lo(b1), bf_hi(b1)};
+        const f32x4 sh = rh - f32x4{bf_lo(b2), bf_hi(b2), bf_lo(b3), bf_hi(b3)};
+        o[0] = u32x4{a0, a1, a2, a3};
+        o[1] = u32x4{b0, b1, b2, b3};
+        o[2] = u32x4{pk_bf16(sl.x, sl.y), pk_bf16(sl.z, sl.w), pk_bf16(sh.x, sh.y), pk_bf16(sh.z, sh.w)};
+    }
+}
+
+template <int P>
+MPCD_DEV f32x4 mma(const u32x4 &a, const u32x4 &b, const f32x4 &c)
+{
+    if constexpr (P == 1)
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                      0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                       0, 0, 0);
+}
+
+// partial product i of the split: (A plane, B plane), smallest first
+constexpr int NPROD(int P) { return P == 1 ? 1 : 6; }
+template <int P> constexpr int PA(int i) { return P == 1 ? 0 : i == 0 ? 2 : i == 1 ? 1 : i == 2 ? 0 : i == 3 ? 1 : 0; }
+template <int P> constexpr int PB(int i) { return P == 1 ? 0 : i == 0 ? 0 : i == 1 ? 1 : i == 2 ? 2 : i == 3 ? 0 : i == 4 ? 1 : 0; }
+
+// (tap, first channel) of lane quarter q in k-chunk kc; cinp is 8, 16 or a multiple of 32
+MPCD_DEV void tap_of(int kc, int q, int cinp, int &tap, int &ci0)
+{
+    if (cinp >= 32) {
+        const int cpt = cinp >> 5;  // chunks per tap
+        tap = kc / cpt;
+        ci0 = (kc - tap * cpt) * 32 + 8 * q;
+    } else {
+        const int tpc = 32 / cinp;  // taps per chunk
+        tap = kc * tpc + (8 * q) / cinp;
+        ci0 = (8 * q) % cinp;
+    }
+}
+
+template <int KIND, int P, int NN, int NC>
+__global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
+{
+    extern __shared__ __attribute__((aligned(16))) char sm[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t r0 = (int64_t)blockIdx.x * a.rb;
+    const int nrow = (int)min((int64_t)a.rb, a.rows - r0);
+    const int win = a.lin + a.halo_l + a.halo_r;
+    const int rowB = win * a.cs, planeB = a.rb * rowB;
+    float *s_stat = reinterpret_cast<float *>(sm + a.stat_off);  // [rb][groups][mean, rstd]
+    float *s_chan = s_stat + 2 * a.rb * 32 + 4;                   // [3][coutp]: gn_w, gn_b, cond
+    if (a.epi != UEPI_BIAS) {
+        for (int c = tid; c < a.coutp; c += MT) {
+            const bool ok = c < a.cout;
+            s_chan[c] = ok ? a.gn_w[c] : 0.f;
+            s_chan[a.coutp + c] = ok ? a.gn_b[c] : 0.f;
+            float cv = 0.f;
+            if (ok && a.epi == UEPI_GN_MISH_COND) cv = a.tp[c] + ((a.cp && !a.cp_stride) ? a.cp[c] : 0.f);
+            s_chan[2 * a.coutp + c] = cv;
+        }
+    }
+
+    // ---- stage the input window, split into P planes (zero outside [0, lin), padded channels, rows >= nrow)
+    const int g8n = a.cinp >> 3, cin = a.ca + a.cb;
+    for (int i = tid; i < a.rb * win * g8n; i += MT) {
+        const int g8 = i % g8n, pw = (i / g8n) % win, r = i / (g8n * win);
+        const int p = pw - a.halo_l, ci = 8 * g8;
+        f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
+        if (r < nrow && p >= 0 && p < a.lin) {
+            const int64_t xr = (r0 + r) % a.x_rows;
+            if ((a.ca & 7) == 0 && ci + 8 <= a.ca) {
+                const float *s = a.xa + ((size_t)xr * a.lin + p) * a.ca + ci;
+                lo = ldg4(s);
+                hi = ldg4(s + 4);
+            } else if ((a.ca & 7) == 0 && (a.cb & 7) == 0 && ci >= a.ca && ci + 8 <= cin) {
+                const float *s = a.xb + ((size_t)xr * a.lin + p) * a.cb + (ci - a.ca);
+                lo = ldg4(s);
+                hi = ldg4(s + 4);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const int c = ci + e;
+                    float v = 0.f;
+                    if (c < a.ca) v = a.xa[((size_t)xr * a.lin + p) * a.ca + c];
+                    else if (c < cin) v = a.xb[((size_t)xr * a.lin + p) * a.cb + (c - a.ca)];
+                    if (e < 4) lo[e] = v; else hi[e - 4] = v;
+                }
+            }
+        }
+        u32x4 o[P];
+        split8<P>(lo, hi, o);
+#pragma unroll
+        for (int pl = 0; pl < P; ++pl)
+            *reinterpret_cast<u32x4 *>(sm + pl * planeB + r * rowB + pw * a.cs + g8 * 16) = o[pl];
+    }
+    __syncthreads();
+
+    // ---- implicit GEMM
+    const int NT = a.coutp >> 4, KC = a.kc;
+    const int npar = KIND == UCONV_UP4 ? 2 : 1;
+    const int nval = KIND == UCONV_UP4 ? a.rb * a.lin : a.rb * a.lout;  // real columns per parity block
+    const int ctp = (nval + 15) >> 4, cpar16 = ctp * 16;
+    const int npj = (NT + NN - 1) / NN, ncg = (ctp + NC - 1) / NC;
+    const int jobs = npj * ncg * npar;
+    const int col = lane & 15, q = lane >> 4;
+    const int sout = a.coutp + 4;
+    float *s_out = reinterpret_cast<float *>(a.alias ? sm : sm + P * planeB);
+
+    const uint64_t wa = (uint64_t)a.w;
+    const uint32_t wlo = __builtin_amdgcn_readfirstlane((uint32_t)wa), whi = __builtin_amdgcn_readfirstlane((uint32_t)(wa >> 32));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(((uint64_t)whi << 32) | wlo), (short)0, (int)(npar * NT * KC * P * 1024), 0x00020000);
+    const int lane16 = lane * 16;
+
+    f32x4 acc[NN][NC];
+    auto compute = [&](int job) {
+        const int np = job % npj, rest = job / npj, cg = rest % ncg, par = rest / ncg;
+        // LDS byte offset of this lane's column window (tap 0 / slot 0, channel 0) per c-tile
+        int bb[NC];
+#pragma unroll
+        for (int cc = 0; cc < NC; ++cc) {
+            int cl = (cg * NC + cc) * 16 + col;
+            if (cl >= nval) cl = 0;  // padding column: any in-bounds window, never stored
+            int r, pos0;
+            if (KIND == UCONV_UP4) {
+                r = cl / a.lin;
+                const int m = cl - r * a.lin;
+                pos0 = par == 0 ? m : m + 1;
+            } else {
+                r = cl / a.lout;
+                const int o = cl - r * a.lout;
+                pos0 = KIND == UCONV_SAME5 ? o - 2 : KIND == UCONV_DOWN3 ? 2 * o - 1 : o;
+            }
+            bb[cc] = r * rowB + (pos0 + a.halo_l) * a.cs;
+        }
+        const int nt0 = np * NN;
+#pragma unroll
+        for (int j = 0; j < NN; ++j) {
+            const int nt = min(nt0 + j, NT - 1);
+            const int n = nt * 16 + 4 * q;
+            f32x4 b;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) b[e] = n + e < a.cout ? a.bias[n + e] : 0.f;
+#pragma unroll
+            for (int cc = 0; cc < NC; ++cc) acc[j][cc] = b;
+        }
+        auto load_a = [&](u32x4 (&A)[NN][P], int kc) {
+#pragma unroll
+            for (int j = 0; j < NN; ++j) {
+                const int nt = min(nt0 + j, NT - 1);
+#pragma unroll
+                for (int pl = 0; pl < P; ++pl) {
+                    const int soff = __builtin_amdgcn_readfirstlane((((par * NT + nt) * KC + kc) * P + pl) * 1024);
+                    A[j][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
+                }
+            }
+        };
+        u32x4 A[NN][P];
+        load_a(A, 0);
+        for (int kc = 0; kc < KC; ++kc) {
+            int tap, ci0;
+            tap_of(kc, q, a.cinp, tap, ci0);
+            const int koff = (KIND == UCONV_UP4 ? -tap : tap) * a.cs + 2 * ci0;
+            u32x4 B[NC][P];
+#pragma unroll
+            for (int cc = 0; cc < NC; ++cc)
+#pragma unroll
+                for (int pl = 0; pl < P; ++pl)
+                    B[cc][pl] = *reinterpret_cast<const u32x4 *>(sm + pl * planeB + bb[cc] + koff);
+            u32x4 An[NN][P];
+            if (kc + 1 < KC) load_a(An, kc + 1);
+#pragma unroll
+            for (int i = 0; i < NPROD(P); ++i)
+#pragma unroll
+                for (int j = 0; j < NN; ++j)
+#pragma unroll
+                    for (int cc = 0; cc < NC; ++cc)
+                        acc[j][cc] = mma<P>(A[j][PA<P>(i)], B[cc][PB<P>(i)], acc[j][cc]);
+            if (kc + 1 < KC) {
+#pragma unroll
+                for (int j = 0; j < NN; ++j)
+#pragma unroll
+                    for (int pl = 0; pl < P; ++pl) A[j][pl] = An[j][pl];
+            }
+        }
+    };
+    auto store = [&](int job) {
+        const int np = job % npj, rest = job / npj, cg = rest % ncg, par = rest / ncg;
+#pragma unroll
+        for (int j = 0; j < NN; ++j) {
+            const int nt = np * NN + j;
+            if (nt >= NT) continue;
+#pragma unroll
+            for (int cc = 0; cc < NC; ++cc) {
+                const int ct = cg * NC + cc;
+                if (ct >= ctp) continue;
+                *reinterpret_cast<f32x4 *>(s_out + (size_t)(par * cpar16 + ct * 16 + col) * sout + nt * 16 + 4 * q) =
+                    acc[j][cc];
+            }
+        }
+    };
+    if (a.alias) {  // one job per wave (host-checked): finish every read of the staged input first
+        if (wave < jobs) compute(wave);
+        __syncthreads();
+        if (wave < jobs) store(wave);
+    } else {
+        for (int job = wave; job < jobs; job += MT / 64) {
+            compute(job);
+            store(job);
+        }
+    }
+    __syncthreads();
+
+    auto colof = [&](int r, int oo) -> int {
+        if (KIND == UCONV_UP4) return (oo & 1) * cpar16 + r * a.lin + (oo >> 1);
+        return r * a.lout + oo;
+    };
+
+    // ---- GroupNorm statistics per (row, group): fp64, shifted by the group's first value, tpp lanes each
+    const int epi = a.epi, gsh = a.cpg_shift;  // cpg = cout / groups = 1 << gsh (host-checked, >= 4)
+    if (epi != UEPI_BIAS) {
+        const int pairs = nrow * a.groups, nq = a.lout << (gsh - 2);  // channel quads per (row, group)
+        int tpp = 1;
+        while (tpp < 64 && tpp * 2 * pairs <= MT) tpp *= 2;
+        const int pi = tid / tpp, sub = tid - pi * tpp;
+        double s1 = 0.0, s2 = 0.0;
+        float ref = 0.f;
+        if (pi < pairs) {
+            const int r = pi / a.groups, g = pi - r * a.groups;
+            const float *base = s_out + (g << gsh);
+            ref = base[(size_t)colof(r, 0) * sout];
+            for (int e = sub; e < nq; e += tpp) {
+                const int oo = e >> (gsh - 2), cc = (e - (oo << (gsh - 2))) * 4;
+                const f32x4 v4 = *reinterpret_cast<const f32x4 *>(base + (size_t)colof(r, oo) * sout + cc);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const double v = (double)v4[k] - (double)ref;
+                    s1 += v;
+                    s2 += v * v;
+                }
+            }
+        }
+        for (int m = 1; m < tpp; m <<= 1) {
+            s1 += __shfl_xor(s1, m);
+            s2 += __shfl_xor(s2, m);
+        }
+        if (pi < pairs && sub == 0) {
+            const double n = (double)(nq * 4), ms = s1 / n;
+            const double var = fmax(s2 / n - ms * ms, 0.0);
+            s_stat[2 * pi] = (float)((double)ref + ms);
+            s_stat[2 * pi + 1] = (float)(1.0 / sqrt(var + 1e-5));
+        }
+        __syncthreads();
+    }
+
+    // ---- epilogue + store: thread per (row, position, channel quad); per-channel operands from LDS
+    const int cq = (a.cout + 3) >> 2;
+    for (int i = tid; i < nrow * a.lout * cq; i += MT) {
+        const int q4 = i % cq, oo = (i / cq) % a.lout, r = i / (cq * a.lout);
+        const int co = 4 * q4;
+        const f32x4 raw = *reinterpret_cast<const f32x4 *>(s_out + (size_t)colof(r, oo) * sout + co);
+        const int64_t grow = r0 + r;
+        f32x4 v = raw;
+        if (epi != UEPI_BIAS) {
+            const int g = co >> gsh;
+            const float mean = s_stat[2 * (r * a.groups + g)], rstd = s_stat[2 * (r * a.groups + g) + 1];
+            const f32x4 gw = *reinterpret_cast<const f32x4 *>(s_chan + co);
+            const f32x4 gb = *reinterpret_cast<const f32x4 *>(s_chan + a.coutp + co);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float scale = rstd * gw[e];
+                const float shift = -scale * mean + gb[e];
+                v[e] = mish(raw[e] * scale + shift);
+            }
+            if (epi == UEPI_GN_MISH_COND) {
+                f32x4 cv = *reinterpret_cast<const f32x4 *>(s_chan + 2 * a.coutp + co);
+                if (a.cp && a.cp_stride) {
+                    const int64_t br = grow / a.b_cand, cand = grow - br * a.b_cand;
+                    if (br == 0) cv = cv + *reinterpret_cast<const f32x4 *>(a.cp + (size_t)cand * a.cp_stride + co);
+                }
+                v = v + cv;
+            }
+            if (epi == UEPI_GN_MISH_RES)
+                v = v + ldg4(a.res + ((size_t)grow * a.lout + oo) * a.cout + co);
+        }
+        float *dst = a.out + ((size_t)grow * a.lout + oo) * a.cout + co;
+        if ((a.cout & 3) == 0) {
+            *reinterpret_cast<f32x4 *>(dst) = v;
+        } else {
+            for (int e = 0; e < 4 && co + e < a.cout; ++e) dst[e] = v[e];
+        }
+    }
+}
+
+// ---- host side
+
+uint16_t bf16_rne(float f)
+{
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // NaN stays NaN
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+float bf16_f(uint16_t h)
+{
+    const uint32_t u = (uint32_t)h << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+uint16_t f16_rne(float f)
+{
+    const _Float16 h = (_Float16)f;  // IEEE round to nearest even
+    uint16_t u;
+    memcpy(&u, &h, 2);
+    return u;
+}
+
+int cinp_of(int cin) { return cin <= 8 ? 8 : cin <= 16 ? 16 : (cin + 31) / 32 * 32; }
+int ks_of(int kind) { return kind == UCONV_SAME5 ? 5 : kind == UCONV_DOWN3 ? 3 : kind == UCONV_UP4 ? 2 : 1; }
+
+struct Tile {
+    int nn, nc;
+};
+constexpr Tile kTiles3[] = {{2, 4}, {1, 8}, {1, 4}};
+constexpr Tile kTiles1[] = {{4, 8}, {2, 8}, {2, 4}, {1, 8}, {1, 4}};
+
+template <int KIND, int P, int NN, int NC>
+hipError_t launch_one(const ConvMK &k, size_t lds, hipStream_t st)
+{
+    static bool set = false;
+    if (!set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&conv_mx_kernel<KIND, P, NN, NC>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        set = true;
+    }
+    const int64_t blocks = (k.rows + k.rb - 1) / k.rb;
+    hipLaunchKernelGGL((conv_mx_kernel<KIND, P, NN, NC>), dim3((unsigned)blocks), dim3(MT), lds, st, k);
+    return hipGetLastError();
+}
+
+template <int KIND, int P>
+hipError_t launch_kind(const ConvMK &k, Tile t, size_t lds, hipStream_t st)
+{
+#define T_(A, B) \
+    if (t.nn == A && t.nc == B) return launch_one<KIND, P, A, B>(k, lds, st);
+    if constexpr (P == 3) {
+        T_(2, 4) T_(1, 8) T_(1, 4)
+    } else {
+        T_(4, 8) T_(2, 8) T_(2, 4) T_(1, 8) T_(1, 4)
+    }
+#undef T_
+    return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+void unet_pack_mx(int kind, int cin, int cout, int planes, const float *w_host, ConvLayer &L,
+                  std::vector<uint16_t> &pack)
+{
+    const int ks = ks_of(kind), cinp = cinp_of(cin);
+    const int coutp = (cout + 15) / 16 * 16, NT = coutp / 16;
+    const int KC = (ks * cinp + 31) / 32, npar = kind == UCONV_UP4 ? 2 : 1;
+    L.cinp8 = cinp;
+    L.kc = KC;
+    const size_t base = pack.size();
+    pack.resize(base + (size_t)npar * NT * KC * planes * 512, 0);
+    for (int par = 0; par < npar; ++par)
+        for (int nt = 0; nt < NT; ++nt)
+            for (int kc = 0; kc < KC; ++kc)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int e = 0; e < 8; ++e) {
+                        const int co = nt * 16 + (lane & 15), k = kc * 32 + 8 * (lane >> 4) + e;
+                        const int tap_slot = k / cinp, ci = k - tap_slot * cinp;
+                        float v = 0.f;
+                        if (co < cout && ci < cin && tap_slot < ks) {
+                            if (kind == UCONV_UP4) {
+                                // ConvTranspose1d k4 s2 p1: even o = 2m uses taps 1 (input m), 3 (m-1); odd o
+                                // uses taps 0 (m+1), 2 (m) - slot 0 / slot 1 in that order
+                                const int tap = par == 0 ? (tap_slot == 0 ? 1 : 3) : (tap_slot == 0 ? 0 : 2);
+                                v = w_host[((size_t)ci * cout + co) * 4 + tap];
+                            } else {
+                                v = w_host[((size_t)co * cin + ci) * ks + tap_slot];
+                            }
+                        }
+                        uint16_t t[3] = {0, 0, 0};
+                        if (planes == 1) {
+                            t[0] = f16_rne(v);
+                        } else {
+                            t[0] = bf16_rne(v);
+                            const float r1 = v - bf16_f(t[0]);
+                            t[1] = bf16_rne(r1);
+                            t[2] = bf16_rne(r1 - bf16_f(t[1]));
+                        }
+                        for (int pl = 0; pl < planes; ++pl)
+                            pack[base + (((((size_t)par * NT + nt) * KC + kc) * planes + pl) * 64 + lane) * 8 + e] =
+                                t[pl];
+                    }
+    L.wmx = reinterpret_cast<const uint16_t *>(base);  // element offset; rebased after upload
+}
+
+hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::string *why)
+{
+    const int cinp = k.cinp, KC = k.kc;
+    const int T = KC * 32 / cinp;  // taps / slots covered by the padded K (zero weights beyond ks)
+    if (kind == UCONV_SAME5) {
+        k.halo_l = 2;
+        k.halo_r = std::max(2, T - 3);
+    } else if (kind == UCONV_DOWN3) {
+        k.halo_l = 1;
+        k.halo_r = std::max(0, T - 3);
+    } else if (kind == UCONV_UP4) {
+        k.halo_l = std::max(1, T - 1);
+        k.halo_r = 1;
+    } else {
+        k.halo_l = 0;
+        k.halo_r = T - 1;
+    }
+    // per-position stride: an odd number of 16-byte units
+    int cs = cinp * 2;
+    if (((cs / 16) & 1) == 0) cs += 16;
+    k.cs = cs;
+    const int win = k.lin + k.halo_l + k.halo_r;
+    const int NT = k.coutp / 16, npar = kind == UCONV_UP4 ? 2 : 1;
+    const int nprod = planes == 1 ? 1 : 6;
+    const Tile *tiles = planes == 1 ? kTiles1 : kTiles3;
+    const int ntiles = planes == 1 ? 5 : 3;
+    const size_t cap = 160 * 1024;
+    double best = 1e30;
+    int best_rb = 0, best_alias = 0;
+    Tile best_t{1, 4};
+    size_t best_lds = 0;
+    for (int rb = 32; rb >= 1; rb /= 2) {
+        if (rb > 1 && (int64_t)rb > k.rows) continue;
+        const int nval = kind == UCONV_UP4 ? rb * k.lin : rb * k.lout;
+        const int ctp = (nval + 15) / 16;
+        const size_t in_b = (size_t)planes * rb * win * cs;
+        const size_t out_b = (size_t)npar * ctp * 16 * (k.coutp + 4) * 4;
+        const size_t stat_b = (size_t)(2 * rb * 32 + 4) * 4 + (size_t)3 * k.coutp * 4;
+        for (int ti = 0; ti < ntiles; ++ti) {
+            const Tile t = tiles[ti];
+            const int jobs = ((NT + t.nn - 1) / t.nn) * ((ctp + t.nc - 1) / t.nc) * npar;
+            const int alias = jobs <= MT / 64;
+            const size_t lds = (alias ? std::max(in_b, out_b) : in_b + out_b) + stat_b;
+            if (lds > cap) continue;
+            // per-row cost: MFMA tile slots of the busiest wave (padding included) + fragment loads
+            const int per_wave = (jobs + 3) / 4;
+            const double cyc = (double)per_wave * KC *
+                                   (t.nn * t.nc * nprod * 16.0 + t.nn * planes * 24.0 + t.nc * planes * 8.0) +
+                               (double)in_b / 64.0 + 600.0;
+            const double cost = cyc / rb;
+            if (cost < best * 0.999) {
+                best = cost;
+                best_rb = rb;
+                best_t = t;
+                best_alias = alias;
+                best_lds = lds;
+            }
+        }
+    }
+    if (!best_rb) {
+        if (why) *why = "UNet mx conv: no tiling fits LDS";
+        return hipErrorInvalidValue;
+    }
+    k.rb = best_rb;
+    k.alias = best_alias;
+    {
+        const int nval = kind == UCONV_UP4 ? best_rb * k.lin : best_rb * k.lout;
+        const size_t in_b = (size_t)planes * best_rb * win * cs;
+        const size_t out_b = (size_t)npar * ((nval + 15) / 16) * 16 * (k.coutp + 4) * 4;
+        k.stat_off = (int)(best_alias ? std::max(in_b, out_b) : in_b + out_b);
+    }
+    if (k.epi != UEPI_BIAS) {
+        const int cpg = k.cout / k.groups;
+        int sh = 0;
+        while ((1 << sh) < cpg) ++sh;
+        if ((1 << sh) != cpg || cpg < 4 || k.groups > 32) {
+            if (why) *why = "UNet mx conv: GroupNorm needs a power-of-two group width >= 4 and <= 32 groups";
+            return hipErrorInvalidValue;
+        }
+        k.cpg_shift = sh;
+    }
+#define K_(KD)                                                                            \
+    if (kind == KD)                                                                       \
+        return planes == 1 ? launch_kind<KD, 1>(k, best_t, best_lds, st)                  \
+                           : launch_kind<KD, 3>(k, best_t, best_lds, st);
+    K_(UCONV_SAME5)
+    K_(UCONV_DOWN3)
+    K_(UCONV_UP4)
+    K_(UCONV_PW1)
+#undef K_
+    return hipErrorInvalidValue;
+}

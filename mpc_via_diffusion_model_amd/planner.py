@@ -41,8 +41,8 @@ class NetSpec:
     dim_mults: tuple = (1, 2, 4)
     time_emb_dim: int = 32
     cfg: bool = True          # 4-arg net with the CFG context mask
-    # GEMM numerics: "f32" exact fp32 MFMA; "f32x3" fp32-accurate split-bf16 MFMA (MLP, shared or no
-    # context; include/mpcd.h MPCD_F32X3); "f16" not built
+    # GEMM numerics (include/mpcd.h mpcd_dtype): "f32" exact fp32 MFMA; "f32x3" fp32-accurate split-bf16
+    # MFMA (MLP: shared or no context; UNet: any); "f16" fp16 operands / fp32 accumulate (UNet, cfg 5)
     dtype: str = "f32"
 
     def desc(self):

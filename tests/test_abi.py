@@ -73,13 +73,14 @@ def test_create_without_gpu_reports_error():
 
 
 def test_gemm_numerics_selection_is_validated():
-    """dtype: f32 and f32x3 (MLP only) accepted; f16 and f32x3 on the U-Net are MPCD_EUNSUP (-5);
+    """dtype: f32 and f32x3 accepted for both nets, f16 for the U-Net only (MLP f16 is MPCD_EUNSUP, -5);
     unknown names are rejected on the host."""
     nt, nf = ctypes.c_int32(), ctypes.c_int64()
     L = N.lib()
     assert N.MPCD_F32X3 == 2
     for spec, want in ((NetSpec("mlp", 2, 32, 4, dtype="f32x3"), 0), (NetSpec("mlp", 2, 32, 4), 0),
-                       (NetSpec("unet", 1, 32, 5, dtype="f32x3"), -5), (NetSpec("mlp", 2, 32, 4, dtype="f16"), -5)):
+                       (NetSpec("unet", 1, 32, 5, dtype="f32x3"), 0), (NetSpec("unet", 4, 64, 12, dtype="f16"), 0),
+                       (NetSpec("mlp", 2, 32, 4, dtype="f16"), -5)):
         d = spec.desc()
         assert L.mpcd_net_param_count(ctypes.byref(d), ctypes.byref(nt), ctypes.byref(nf)) == want, spec
     with pytest.raises(ValueError):
