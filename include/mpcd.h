@@ -206,6 +206,26 @@ int mpcd_control_step(mpcd_ctx *ctx, const mpcd_system_desc *sys, double *x_dev,
                       const float *umax_host, const int32_t *flags_dev, int32_t select_first, int32_t decimals,
                       double *u_applied, int64_t *best_index, double *best_cost, void *hip_stream);
 
+/* ---- Candidate-batch data parallelism over RCCL / xGMI. One process per GPU, one
+ * communicator per context; rank r owns global candidates [r*B_local, (r+1)*B_local). The reference has
+ * no distributed code: these entry points are new design, not replacements. */
+#define MPCD_COMM_ID_BYTES 128
+/* Rank 0 creates the id (ncclGetUniqueId) and ships its 128 bytes to every rank out of band. */
+int mpcd_comm_unique_id(void *id_out);
+int mpcd_comm_init(mpcd_ctx *ctx, int32_t nranks, int32_t rank, const void *id);
+int mpcd_comm_info(mpcd_ctx *ctx, int32_t *nranks, int32_t *rank);  /* 1, 0 without mpcd_comm_init */
+/* recv [nranks * count_per_rank] (rank order); without a communicator: a device copy. */
+int mpcd_allgather_f32(mpcd_ctx *ctx, const float *send, float *recv, size_t count_per_rank, void *hip_stream);
+int mpcd_allgather_f64(mpcd_ctx *ctx, const double *send, double *recv, size_t count_per_rank, void *hip_stream);
+int mpcd_broadcast_f32(mpcd_ctx *ctx, float *buf, size_t count, int32_t root, void *hip_stream);
+int mpcd_allreduce_max_i32(mpcd_ctx *ctx, int32_t *buf, size_t count, void *hip_stream);  /* OR of clip flags */
+/* The per-control-step exchange, device-resident end to end (no host round trip): all-gather the fp64
+ * costs into costs_all [nranks * n_local], global argmin (torch.argmin(cost_all), inference_(mpd).py:335-338;
+ * NaN = +inf, lowest global index on ties) into *best_dev, and the winner's row [row_len] (its normalised
+ * [H][d] trajectory) into row_out on every rank (owner writes it, the others zeros, sum all-reduce). */
+int mpcd_select(mpcd_ctx *ctx, const double *cost_local, int64_t n_local, const float *rows_local, int32_t row_len,
+                double *costs_all, mpcd_best *best_dev, float *row_out, void *hip_stream);
+
 /* Timing of the last mpcd_sample's main kernel (HIP events on the call's stream), milliseconds.
  * Blocks until that kernel has finished. */
 int mpcd_last_sample_ms(mpcd_ctx *ctx, float *ms);

@@ -17,6 +17,7 @@ MPCD_NET_MLP, MPCD_NET_UNET = 1, 2
 MPCD_F32, MPCD_F16, MPCD_F32X3 = 0, 1, 2
 MPCD_DDPM_CFG, MPCD_DDIM_CFG, MPCD_DDIM = 0, 1, 2
 MPCD_COST_CANONICAL, MPCD_COST_CALMPC = 0, 1
+MPCD_COMM_ID_BYTES = 128
 
 _STATUS = {-1: "EINVAL", -2: "EHIP", -3: "ESTATE", -4: "ENOMEM", -5: "EUNSUP"}
 
@@ -82,6 +83,18 @@ EXPORTS = {
                            ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                            ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                            ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "mpcd_comm_unique_id": ([ctypes.c_void_p], ctypes.c_int),
+    "mpcd_comm_init": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p], ctypes.c_int),
+    "mpcd_comm_info": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+    "mpcd_allgather_f32": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p],
+                           ctypes.c_int),
+    "mpcd_allgather_f64": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p],
+                           ctypes.c_int),
+    "mpcd_broadcast_f32": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32, ctypes.c_void_p],
+                           ctypes.c_int),
+    "mpcd_allreduce_max_i32": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
+    "mpcd_select": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
+                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
 }
 
 _lib = None

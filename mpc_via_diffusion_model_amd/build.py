@@ -23,6 +23,10 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={AR
          "-Wno-unused-function", "-Wno-unused-variable"]
 
 
+ROCM_LIB = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib")
+LIBS = [f"-L{ROCM_LIB}", "-lrccl", f"-Wl,-rpath,{ROCM_LIB}"]  # RCCL: the C ABI's candidate-batch exchange
+
+
 def hipcc():
     for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if c and os.path.exists(c):
@@ -67,7 +71,7 @@ def build(force=False, verbose=False, variant=None, defines=()):
         list(ex.map(run, jobs))
     objs = [os.path.join(obj, s.replace(".hip", ".o")) for s in SOURCES]
     if force or jobs or _stale(out, objs):
-        run([cc, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", out] + objs)
+        run([cc, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", out] + objs + LIBS)
     return out
 
 

@@ -11,6 +11,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/mpcd.h"
 #include "internal.h"
 #include "unet.h"
@@ -29,6 +31,8 @@ hipError_t launch_control_step(const mpcd_system_desc &d, double *x_dev, int64_t
                                const int *flags_dev, int select_first, int decimals, double *u_applied,
                                int64_t *best_idx, double *best_cost, hipStream_t stream);
 hipError_t launch_argmin(const double *cost, int64_t n, int64_t offset, mpcd_best *best, hipStream_t stream);
+hipError_t launch_winner_row(const mpcd_best *best, int64_t lo, int64_t n_local, const float *rows, int row_len,
+                             float *out, hipStream_t stream);
 
 namespace {
 
@@ -232,6 +236,9 @@ struct mpcd_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     float *dbg = nullptr;  // debug dump target for mpcd_eps (mpcd_debug_set)
+    // candidate-batch data parallelism: one RCCL communicator per context (mpcd_comm_init)
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
 };
 
 namespace {
@@ -481,6 +488,7 @@ void mpcd_destroy(mpcd_ctx *c)
         b->release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
     delete c;
 }
 
@@ -817,6 +825,99 @@ int mpcd_argmin(mpcd_ctx *c, const double *cost, int64_t n, int64_t offset, mpcd
     hipStream_t st = static_cast<hipStream_t>(stream_ptr);
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(launch_argmin(cost, n, offset, best, st));
+    return MPCD_OK;
+}
+
+// ---- candidate-batch data parallelism over RCCL
+
+#define NCCL_TRY(expr)                                                                          \
+    do {                                                                                        \
+        ncclResult_t r_ = (expr);                                                               \
+        if (r_ != ncclSuccess) return fail(MPCD_EHIP, "%s: %s", #expr, ncclGetErrorString(r_)); \
+    } while (0)
+
+int mpcd_comm_unique_id(void *id_out)
+{
+    if (!id_out) return fail(MPCD_EINVAL, "null argument");
+    static_assert(sizeof(ncclUniqueId) == MPCD_COMM_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    memcpy(id_out, &id, sizeof id);
+    return MPCD_OK;
+}
+
+int mpcd_comm_init(mpcd_ctx *c, int32_t nranks, int32_t rank, const void *id_in)
+{
+    if (!c || !id_in || nranks < 1 || rank < 0 || rank >= nranks) return fail(MPCD_EINVAL, "bad comm arguments");
+    if (c->comm) return fail(MPCD_ESTATE, "communicator already initialised");
+    HIP_TRY(hipSetDevice(c->device));
+    ncclUniqueId id;
+    memcpy(&id, id_in, sizeof id);
+    NCCL_TRY(ncclCommInitRank(&c->comm, nranks, id, rank));
+    c->nranks = nranks;
+    c->rank = rank;
+    return MPCD_OK;
+}
+
+int mpcd_comm_info(mpcd_ctx *c, int32_t *nranks, int32_t *rank)
+{
+    if (!c || !nranks || !rank) return fail(MPCD_EINVAL, "null argument");
+    *nranks = c->nranks;
+    *rank = c->rank;
+    return MPCD_OK;
+}
+
+static int comm_gather(mpcd_ctx *c, const void *send, void *recv, size_t count, ncclDataType_t t, size_t esz,
+                       hipStream_t st)
+{
+    HIP_TRY(hipSetDevice(c->device));
+    if (!c->comm) {  // single rank: the gather is a copy
+        if (send != recv) HIP_TRY(hipMemcpyAsync(recv, send, count * esz, hipMemcpyDeviceToDevice, st));
+        return MPCD_OK;
+    }
+    NCCL_TRY(ncclAllGather(send, recv, count, t, c->comm, st));
+    return MPCD_OK;
+}
+
+int mpcd_allgather_f32(mpcd_ctx *c, const float *send, float *recv, size_t count_per_rank, void *stream)
+{
+    if (!c || !send || !recv) return fail(MPCD_EINVAL, "null argument");
+    return comm_gather(c, send, recv, count_per_rank, ncclFloat32, 4, static_cast<hipStream_t>(stream));
+}
+
+int mpcd_allgather_f64(mpcd_ctx *c, const double *send, double *recv, size_t count_per_rank, void *stream)
+{
+    if (!c || !send || !recv) return fail(MPCD_EINVAL, "null argument");
+    return comm_gather(c, send, recv, count_per_rank, ncclFloat64, 8, static_cast<hipStream_t>(stream));
+}
+
+int mpcd_broadcast_f32(mpcd_ctx *c, float *buf, size_t count, int32_t root, void *stream)
+{
+    if (!c || !buf || root < 0 || root >= c->nranks) return fail(MPCD_EINVAL, "bad broadcast arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->comm) NCCL_TRY(ncclBroadcast(buf, buf, count, ncclFloat32, root, c->comm, static_cast<hipStream_t>(stream)));
+    return MPCD_OK;
+}
+
+int mpcd_allreduce_max_i32(mpcd_ctx *c, int32_t *buf, size_t count, void *stream)
+{
+    if (!c || !buf) return fail(MPCD_EINVAL, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->comm) NCCL_TRY(ncclAllReduce(buf, buf, count, ncclInt32, ncclMax, c->comm, static_cast<hipStream_t>(stream)));
+    return MPCD_OK;
+}
+
+int mpcd_select(mpcd_ctx *c, const double *cost_local, int64_t n_local, const float *rows_local, int32_t row_len,
+                double *costs_all, mpcd_best *best_dev, float *row_out, void *stream)
+{
+    if (!c || !cost_local || !rows_local || !costs_all || !best_dev || !row_out || n_local < 1 || row_len < 1)
+        return fail(MPCD_EINVAL, "bad select arguments");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    int rc = comm_gather(c, cost_local, costs_all, (size_t)n_local, ncclFloat64, 8, st);
+    if (rc) return rc;
+    HIP_TRY(launch_argmin(costs_all, n_local * c->nranks, 0, best_dev, st));
+    HIP_TRY(launch_winner_row(best_dev, (int64_t)c->rank * n_local, n_local, rows_local, row_len, row_out, st));
+    if (c->comm) NCCL_TRY(ncclAllReduce(row_out, row_out, (size_t)row_len, ncclFloat32, ncclSum, c->comm, st));
     return MPCD_OK;
 }
 

@@ -343,7 +343,24 @@ __global__ __launch_bounds__(1024) void argmin_kernel(const double *cost, int64_
     }
 }
 
+// The selection exchange without a host round trip: every rank writes the winner's row if it owns
+// it and zeros otherwise; a sum all-reduce then hands every rank the winner's row exactly (x + 0 = x).
+__global__ void winner_row_kernel(const mpcd_best *best, int64_t lo, int64_t n_local, const float *rows, int row_len,
+                                  float *out)
+{
+    const int64_t idx = best->index - lo;
+    const bool own = idx >= 0 && idx < n_local;
+    for (int i = threadIdx.x; i < row_len; i += blockDim.x) out[i] = own ? rows[idx * row_len + i] : 0.f;
+}
+
 }  // namespace
+
+hipError_t launch_winner_row(const mpcd_best *best, int64_t lo, int64_t n_local, const float *rows, int row_len,
+                             float *out, hipStream_t stream)
+{
+    hipLaunchKernelGGL(winner_row_kernel, dim3(1), dim3(256), 0, stream, best, lo, n_local, rows, row_len, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_clip_flag(const float *x, int64_t n, int *flag_dev, hipStream_t stream)
 {

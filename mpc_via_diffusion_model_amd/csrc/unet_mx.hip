@@ -112,15 +112,20 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
     const int win = a.lin + a.halo_l + a.halo_r;
     const int rowB = win * a.cs, planeB = a.rb * rowB;
     float *s_stat = reinterpret_cast<float *>(sm + a.stat_off);  // [rb][groups][mean, rstd]
-    float *s_chan = s_stat + 2 * a.rb * 32 + 4;                   // [3][coutp]: gn_w, gn_b, cond
+    // [4][coutp]: gn_w, gn_b, cond of the context rows (tproj + shared cproj), cond of the masked rows (tproj)
+    float *s_chan = s_stat + 2 * a.rb * 32 + 4;
     if (a.epi != UEPI_BIAS) {
         for (int c = tid; c < a.coutp; c += MT) {
             const bool ok = c < a.cout;
             s_chan[c] = ok ? a.gn_w[c] : 0.f;
             s_chan[a.coutp + c] = ok ? a.gn_b[c] : 0.f;
-            float cv = 0.f;
-            if (ok && a.epi == UEPI_GN_MISH_COND) cv = a.tp[c] + ((a.cp && !a.cp_stride) ? a.cp[c] : 0.f);
-            s_chan[2 * a.coutp + c] = cv;
+            float cu = 0.f, cc = 0.f;
+            if (ok && a.epi == UEPI_GN_MISH_COND) {
+                cu = a.tp[c];
+                cc = (a.cp && !a.cp_stride) ? cu + a.cp[c] : cu;
+            }
+            s_chan[2 * a.coutp + c] = cc;
+            s_chan[3 * a.coutp + c] = cu;
         }
     }
 
@@ -336,12 +341,11 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
                 const float shift = -scale * mean + gb[e];
                 v[e] = mish(raw[e] * scale + shift);
             }
-            if (epi == UEPI_GN_MISH_COND) {
-                f32x4 cv = *reinterpret_cast<const f32x4 *>(s_chan + 2 * a.coutp + co);
-                if (a.cp && a.cp_stride) {
-                    const int64_t br = grow / a.b_cand, cand = grow - br * a.b_cand;
-                    if (br == 0) cv = cv + *reinterpret_cast<const f32x4 *>(a.cp + (size_t)cand * a.cp_stride + co);
-                }
+            if (epi == UEPI_GN_MISH_COND) {  // row < b_cand: context branch; else the masked (CFG) branch
+                const int64_t br = grow / a.b_cand, cand = grow - br * a.b_cand;
+                f32x4 cv = *reinterpret_cast<const f32x4 *>(s_chan + (br == 0 ? 2 : 3) * a.coutp + co);
+                if (a.cp && a.cp_stride && br == 0)
+                    cv = cv + *reinterpret_cast<const f32x4 *>(a.cp + (size_t)cand * a.cp_stride + co);
                 v = v + cv;
             }
             if (epi == UEPI_GN_MISH_RES)
@@ -502,7 +506,7 @@ hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::
         const int ctp = (nval + 15) / 16;
         const size_t in_b = (size_t)planes * rb * win * cs;
         const size_t out_b = (size_t)npar * ctp * 16 * (k.coutp + 4) * 4;
-        const size_t stat_b = (size_t)(2 * rb * 32 + 4) * 4 + (size_t)3 * k.coutp * 4;
+        const size_t stat_b = (size_t)(2 * rb * 32 + 4) * 4 + (size_t)4 * k.coutp * 4;
         for (int ti = 0; ti < ntiles; ++ti) {
             const Tile t = tiles[ti];
             const int jobs = ((NT + t.nn - 1) / t.nn) * ((ctp + t.nc - 1) / t.nc) * npar;

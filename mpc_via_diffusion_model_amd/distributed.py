@@ -6,11 +6,20 @@ results do not depend on the sharding). The one exchange per control step:
   1. all-gather of the per-candidate fp64 costs (B_local per rank)      -> every rank
   2. global argmin on every rank (NaN = +inf, lowest index on ties)     -> identical on all ranks
   3. broadcast of the winner's normalised [H, d] row from its owner     -> every rank
-Works on any torch.distributed backend: "nccl" (= RCCL on ROCm) with device tensors, or "gloo"
-with CPU tensors (the CPU tests). Weights, schedule and x0 are replicated, not exchanged.
+Two interchangeable implementations of that exchange:
+  * select()/any_flag() below: torch.distributed collectives - any backend: "nccl" (= RCCL on ROCm)
+    with device tensors, or "gloo" with CPU tensors (the CPU tests);
+  * NativeComm: the communicator inside libmpcd.so (mpcd_comm_init, RCCL over xGMI) and mpcd_select,
+    which keeps the whole exchange on the device - all-gather, argmin, and the winner's row handed to
+    every rank by a sum all-reduce of (row if owner else zeros) - with no host round trip in between.
+Weights, schedule and x0 are replicated, not exchanged.
 """
+import ctypes
+
 import torch
 import torch.distributed as dist
+
+from . import _native as N
 
 
 def world(group=None):
@@ -72,3 +81,48 @@ def select(cost_local, rows_local, argmin, group=None):
     owner, local = divmod(idx, n_local)
     row = broadcast_row(rows_local[local if owner == rank else 0], owner, group)
     return idx, best, row, costs
+
+
+class NativeComm:
+    """RCCL communicator owned by a planner's libmpcd context (one process per GPU). Rank 0 creates the
+    128-byte unique id; it is shipped to the other ranks over the torch.distributed group (any backend).
+    Without an initialised process group (or with one rank) no communicator is made and the calls
+    reduce to their single-rank forms inside the library."""
+
+    def __init__(self, plan, group=None):
+        self.plan, self.group = plan, group
+        self.rank, self.size = world(group)
+        L = N.lib()
+        if self.size > 1:
+            uid = (ctypes.c_uint8 * N.MPCD_COMM_ID_BYTES)()
+            if self.rank == 0:
+                N.check(L.mpcd_comm_unique_id(uid), "mpcd_comm_unique_id")
+            obj = [bytes(uid)]
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            dist.broadcast_object_list(obj, src=src, group=group)
+            uid = (ctypes.c_uint8 * N.MPCD_COMM_ID_BYTES).from_buffer_copy(obj[0])
+            N.check(L.mpcd_comm_init(plan._ctx, self.size, self.rank, uid), "mpcd_comm_init")
+        nr, rk = ctypes.c_int32(), ctypes.c_int32()
+        N.check(L.mpcd_comm_info(plan._ctx, ctypes.byref(nr), ctypes.byref(rk)), "mpcd_comm_info")
+        assert (nr.value, rk.value) == ((self.size, self.rank) if self.size > 1 else (1, 0))
+        self._best = torch.zeros(2, dtype=torch.float64, device=plan.device)
+
+    def any_flag(self, flag_local):
+        t = flag_local.clone()
+        N.check(N.lib().mpcd_allreduce_max_i32(self.plan._ctx, ctypes.c_void_p(t.data_ptr()), t.numel(),
+                                               self.plan._stream()), "mpcd_allreduce_max_i32")
+        return t
+
+    def select(self, cost_local, rows_local):
+        """Same contract as select(): (global index, cost, winner row, all costs)."""
+        n_local = cost_local.shape[0]
+        row_shape = rows_local.shape[1:]
+        row_len = rows_local[0].numel()
+        costs = torch.empty(self.size * n_local, dtype=torch.float64, device=cost_local.device)
+        row = torch.empty(row_len, dtype=torch.float32, device=cost_local.device)
+        N.check(N.lib().mpcd_select(self.plan._ctx, ctypes.c_void_p(cost_local.contiguous().data_ptr()), n_local,
+                                    ctypes.c_void_p(rows_local.contiguous().data_ptr()), row_len,
+                                    ctypes.c_void_p(costs.data_ptr()), ctypes.c_void_p(self._best.data_ptr()),
+                                    ctypes.c_void_p(row.data_ptr()), self.plan._stream()), "mpcd_select")
+        host = self._best.cpu()
+        return int(host.view(torch.int64)[1]), float(host[0]), row.view(row_shape), costs

@@ -356,9 +356,11 @@ class DiffusionMPC:
                                 cost=cs.t().cpu().numpy(), index=ix.t().cpu().numpy())
 
     def mpc_step(self, x0, system: System, n_samples, w=0.01, sample_fn="ddpm_cfg", n_wo_noise=0, ddim_steps=None,
-                 clamp_x0=False, seed=0, noise=None, group=None):
+                 clamp_x0=False, seed=0, noise=None, group=None, comm=None):
         """One control step: sample n_samples candidates on this rank (weak scaling: every rank adds
-        n_samples), roll out + cost them, all-gather costs, pick the global argmin, broadcast it."""
+        n_samples), roll out + cost them, all-gather costs, pick the global argmin, broadcast it.
+        comm: a distributed.NativeComm (the exchange inside libmpcd.so over RCCL) or None
+        (torch.distributed collectives on `group`)."""
         rank, size = D.world(group)
         offset, total = D.shard(n_samples, group)
         ctx = torch.from_numpy(self.normalize_condition(x0)[None])
@@ -372,9 +374,12 @@ class DiffusionMPC:
         elif sampler == N.MPCD_DDPM_CFG and self.ddpm_final_in_range:
             flag = torch.zeros(1, dtype=torch.int32, device=self.device)
         else:
-            flag = D.any_flag(self.clip_flag(u_norm), group)
+            flag = comm.any_flag(self.clip_flag(u_norm)) if comm else D.any_flag(self.clip_flag(u_norm), group)
         cost_local = self.rollout_cost(system, x0, u_norm, flag)
-        idx, best, row, costs = D.select(cost_local, u_norm, self.argmin, group)
+        if comm is not None:
+            idx, best, row, costs = comm.select(cost_local, u_norm)
+        else:
+            idx, best, row, costs = D.select(cost_local, u_norm, self.argmin, group)
         u_best = self.unnormalize_states(row[None], flag)[0]
         u_host = u_best.cpu().numpy()
         return MPCResult(u0=u_host[0].copy(), u_best=u_host, best_cost=best, best_index=idx, costs=costs,

@@ -1,10 +1,10 @@
-# U-Net mx kernels: parity tests, then throughput per GEMM numerics (+ kernel-trace of the x3 run)
+# U-Net mx kernels + comm: parity tests, then throughput per GEMM numerics (+ kernel-trace of the x3 run)
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof_unet_mx
-timeout -k 10 400 python -u -m pytest tests/test_gpu_unet.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_unet.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_unet.py tests/test_gpu_comm.py -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_unet.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_unet.log; if [ $rc -gt 1 ]; then exit $rc; fi
-for dt in f32x3 f16 f32; do
+for dt in f32x3 f16; do
   timeout -k 10 200 python tools/unet_perf.py --B 16384 --H 32 --C 2 --steps 10 --dtype $dt >> gpurun_out/unet_perf.log 2>&1 || exit $?
   timeout -k 10 200 python tools/unet_perf.py --B 8192 --H 64 --C 5 --steps 5 --dtype $dt >> gpurun_out/unet_perf.log 2>&1 || exit $?
 done
