@@ -12,11 +12,12 @@ ap.add_argument("--C", type=int, default=2)
 ap.add_argument("--N", type=int, default=100)
 ap.add_argument("--steps", type=int, default=10, help="DDIM sampling steps (network evaluations)")
 ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--schedule", default="exponential")
 ap.add_argument("--dtype", default="f32x3", choices=["f32", "f32x3", "f16"])
 a = ap.parse_args()
 torch.manual_seed(0)
 net = nets.ConditionedTemporalUnet(state_dim=a.d, context_dim=a.C)
-plan = DiffusionMPC(NetSpec("unet", a.d, a.H, a.C, dtype=a.dtype), net.state_dict(), n_diffusion_steps=a.N)
+plan = DiffusionMPC(NetSpec("unet", a.d, a.H, a.C, dtype=a.dtype), net.state_dict(), variance_schedule=a.schedule, n_diffusion_steps=a.N)
 ctx = torch.rand(1, a.C) * 2 - 1
 plan.sample_trajectories(ctx, a.B, a.H, sample_fn="ddim_cfg", ddim_steps=2)
 torch.cuda.synchronize()
@@ -26,7 +27,7 @@ for _ in range(a.reps):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     evals = a.steps + 1
-    mac = {32: 9122560, 64: 18209152}.get(a.H, 0) + 896 * (a.C - 5)
+    mac = {32: 9122560, 64: 18209152}.get(a.H, 0) + 896 * (a.C - 5) + 224 * a.H * (a.d - 1)
     fl = a.B * evals * 2 * 2 * mac
     print(f"{a.dtype} B={a.B} H={a.H}: {el*1e3:.1f} ms for {evals} CFG net evals -> {el/evals*1e3:.2f} ms/eval, "
           f"{fl/el/1e12:.1f} TFLOP/s, {a.B/el*evals/101:.0f} cand/s at 101 evals")
