@@ -87,6 +87,7 @@ def main():
         torch.cuda.set_device(0)
 
     from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec, systems
+    from mpc_via_diffusion_model_amd import distributed as D
     from oracle import nets  # random-init weights of the net's architecture (seed 0), test infra only
 
     torch.manual_seed(0)
@@ -98,8 +99,11 @@ def main():
     rng = np.random.default_rng(1)
     x0s = rng.uniform(-1, 1, (args.warmup + args.steps, system.n_x))
 
-    def step(i):
-        return plan.mpc_step(x0s[i], system, CFG["B"], w=CFG["w"], seed=2 + i)
+    # the per-step exchange runs inside libmpcd.so (RCCL communicator of the planner's context)
+    comm = D.NativeComm(plan) if world > 1 else None
+
+    def step(i):  # one mpcd_mpc_step call: sample, clip flag, rollout/cost, select, one D2H copy
+        return plan.mpc_step(x0s[i], system, CFG["B"], w=CFG["w"], seed=2 + i, comm=comm)
 
     for i in range(args.warmup):
         step(i)

@@ -44,11 +44,12 @@ enum mpcd_net_kind {
 
 /* GEMM numerics of the noise-net.
  * MPCD_F32:   exact fp32 MFMA (v_mfma_f32_16x16x4_f32: one rounding per product, an fmaf chain).
- * MPCD_F16:   fp16 hidden activations (SURVEY cfg 5) - not built, MPCD_EUNSUP.
- * MPCD_F32X3: fp32-accurate split-bf16 MFMA (MLP only): each fp32 operand = three bf16 terms, the six
+ * MPCD_F16:   fp16 GEMM operands with fp32 accumulation on v_mfma_f32_16x16x32_f16 (SURVEY cfg 5,
+ *             "fp16 hidden with MFMA GEMM"); U-Net only (an MLP net returns MPCD_EUNSUP).
+ * MPCD_F32X3: fp32-accurate split-bf16 MFMA (MLP and U-Net): each fp32 operand = three bf16 terms, the six
  *             partial products >= 2^-16 of the leading one accumulated in fp32 (error at the level of
- *             the fp32 MFMA's). Needs a context shared by all candidates (or none); a per-candidate
- *             context runs the MPCD_F32 kernel. */
+ *             the fp32 MFMA's). MLP: needs a context shared by all candidates (or none); a
+ *             per-candidate context runs the MPCD_F32 kernel. */
 enum mpcd_dtype { MPCD_F32 = 0, MPCD_F16 = 1, MPCD_F32X3 = 2 };
 
 typedef struct {
@@ -225,6 +226,30 @@ int mpcd_allreduce_max_i32(mpcd_ctx *ctx, int32_t *buf, size_t count, void *hip_
  * [H][d] trajectory) into row_out on every rank (owner writes it, the others zeros, sum all-reduce). */
 int mpcd_select(mpcd_ctx *ctx, const double *cost_local, int64_t n_local, const float *rows_local, int32_t row_len,
                 double *costs_all, mpcd_best *best_dev, float *row_out, void *hip_stream);
+
+/* ---- One control step in one call: the whole per-step path of Diffusion_MPC_Inference.py:229-262 /
+ * Cart_Diffusion_inference.py:439-470 (normalize_condition -> run_CFG -> unnormalize_states -> cost of
+ * every candidate -> argmin -> applied action) for this rank's shard, plus the exchange of mpcd_select
+ * when the context has a communicator. Everything stays on the device until one D2H copy of the
+ * result; the call then synchronises the stream, so best_host / u_best_host are valid on return. */
+typedef struct {
+    const mpcd_system_desc *sys;   /* n_u == the net's state_dim */
+    const double *x0;              /* host [n_x] fp64 plant state */
+    const float *ctx_min, *ctx_max; /* host [C] condition limits: ctx = fp32(2*((x0-min)/fp32(max-min)) - 1) in fp64
+                                      (LimitsNormalizer.normalize, normalization.py:149-154) */
+    const float *act_min, *act_max; /* host [d] action limits (LimitsNormalizer.unnormalize, :156-167) */
+    mpcd_sample_args sample;       /* .context / .context_shared are ignored (the normalised x0 is the shared
+                                      context); .batch = B_local; .global_offset = rank * B_local; .x_out required */
+    int32_t flag_zero;             /* 1: the caller has proven the global clip flag 0 (DDPM whose last posterior
+                                      mean cannot leave [-1, 1]) - no flag reduction is run */
+    double *cost_local;            /* dev [batch] fp64 costs of this rank's candidates (out) */
+    double *costs_all;             /* dev [nranks * batch] all costs (out), needed with a communicator, else unused */
+} mpcd_step_args;
+
+/* best_host: global winner (index over all ranks); u_best_host: host [H*d] fp32, the winner's
+ * UNnormalised trajectory (u_best[0] is the applied action before the reference's rounding). */
+int mpcd_mpc_step(mpcd_ctx *ctx, const mpcd_step_args *args, mpcd_best *best_host, float *u_best_host,
+                  void *hip_stream);
 
 /* Timing of the last mpcd_sample's main kernel (HIP events on the call's stream), milliseconds.
  * Blocks until that kernel has finished. */

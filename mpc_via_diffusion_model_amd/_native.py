@@ -48,6 +48,13 @@ class Best(ctypes.Structure):
     _fields_ = [("cost", ctypes.c_double), ("index", ctypes.c_int64)]
 
 
+class StepArgs(ctypes.Structure):
+    _fields_ = [("sys", ctypes.POINTER(SystemDesc)), ("x0", ctypes.c_void_p), ("ctx_min", ctypes.c_void_p),
+                ("ctx_max", ctypes.c_void_p), ("act_min", ctypes.c_void_p), ("act_max", ctypes.c_void_p),
+                ("sample", SampleArgs), ("flag_zero", ctypes.c_int32), ("cost_local", ctypes.c_void_p),
+                ("costs_all", ctypes.c_void_p)]
+
+
 EXPORTS = {
     "mpcd_net_param_count": ([ctypes.POINTER(NetDesc), ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)],
                              ctypes.c_int),
@@ -93,6 +100,8 @@ EXPORTS = {
     "mpcd_broadcast_f32": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32, ctypes.c_void_p],
                            ctypes.c_int),
     "mpcd_allreduce_max_i32": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
+    "mpcd_mpc_step": ([ctypes.c_void_p, ctypes.POINTER(StepArgs), ctypes.POINTER(Best), ctypes.c_void_p,
+                       ctypes.c_void_p], ctypes.c_int),
     "mpcd_select": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
 }

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/mpcd.h"
 #include "common.h"
 
 // One conditioning Linear (cond_mlp.1 of a residual / MLP block): out width `width`, weight
@@ -49,3 +50,15 @@ hipError_t launch_mlp_sampler(int d0, int nb, const MlpSampleArgs &a, hipStream_
 int mlp_packed_floats_x3(int d0);
 void mlp_pack_weights_x3(int d0, const float *const *lin_w, const float *const *lin_b, float *out);
 hipError_t launch_mlp_x3(int d0, int nb, const MlpSampleArgs &a, hipStream_t stream);
+
+// Fused selection for launch_rollout_cost (single rank): see rollout.hip SelectK
+struct RolloutSelect {
+    mpcd_best *best;
+    float *row_out;
+    double *part_cost;
+    int64_t *part_idx;
+    unsigned *counter;    // zero-initialised, reset by the kernel
+    int64_t n_part;       // capacity of part_* (>= ceil(batch / 64))
+    int64_t offset;
+};
+constexpr int kRolloutBlock = 64;  // candidates per rollout workgroup

@@ -17,12 +17,13 @@
 #include "internal.h"
 #include "unet.h"
 
-hipError_t launch_clip_flag(const float *x, int64_t n, int *flag_dev, hipStream_t stream);
+hipError_t launch_clip_flag(const float *x, int64_t n, int *flag_dev, unsigned *ws, hipStream_t stream);
 hipError_t launch_unnormalize(const float *x, int64_t n, int dim, const int *flag_dev, const float *mn_host,
                               const float *mx_host, float *out, hipStream_t stream);
 hipError_t launch_rollout_cost(const mpcd_system_desc &d, const double *x0_host, const double *x0_dev, int64_t group,
                                const float *u_norm, const float *umin_host, const float *umax_host, const int *flag_dev,
-                               int64_t batch, int H, double *cost, hipStream_t stream);
+                               int64_t batch, int H, double *cost, hipStream_t stream,
+                               const RolloutSelect *sel = nullptr);
 hipError_t launch_clip_flags(const float *x, int64_t n_groups, int64_t group_elems, int *flags_dev, hipStream_t stream);
 hipError_t launch_normalize_states(const double *x, int64_t M, int C, const float *mn_host, const float *mx_host,
                                    float *out, hipStream_t stream);
@@ -239,6 +240,13 @@ struct mpcd_ctx {
     // candidate-batch data parallelism: one RCCL communicator per context (mpcd_comm_init)
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    // flag: [0] internal clip flag, [16..] zero-initialised counters of the self-resetting reductions
+    unsigned *sync_ws() const { return flag.as<unsigned>() + 16; }
+    // mpcd_mpc_step: device context row, per-block argmin partials, {best, winner row} result block
+    // and its pinned host mirror (one D2H copy per control step)
+    DevBuf step_ctx, step_part, step_out;
+    void *step_host = nullptr;
+    size_t step_host_bytes = 0;
 };
 
 namespace {
@@ -471,9 +479,14 @@ int mpcd_create(int device, mpcd_ctx **out)
         delete c;
         return fail(MPCD_EHIP, "hipEventCreate failed");
     }
-    if (int rc = c->flag.ensure(64)) {
+    if (int rc = c->flag.ensure(256)) {
         delete c;
         return rc;
+    }
+    if (hipMemset(c->flag.p, 0, 256) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        c->flag.release();
+        delete c;
+        return fail(MPCD_EHIP, "hipMemset of the reduction counters failed");
     }
     *out = c;
     return MPCD_OK;
@@ -484,11 +497,12 @@ void mpcd_destroy(mpcd_ctx *c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (DevBuf *b : {&c->params, &c->wpack, &c->wpack3, &c->cond_layers, &c->unet_pack, &c->plan, &c->tproj, &c->cproj, &c->flag,
-                      &c->unet_ws})
+                      &c->unet_ws, &c->step_ctx, &c->step_part, &c->step_out})
         b->release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->step_host) (void)hipHostFree(c->step_host);
     delete c;
 }
 
@@ -715,7 +729,7 @@ int mpcd_clip_flag(mpcd_ctx *c, const float *x, int64_t n, int32_t *flag, void *
 {
     if (!c || !x || !flag || n < 1) return fail(MPCD_EINVAL, "bad clip_flag arguments");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(launch_clip_flag(x, n, flag, static_cast<hipStream_t>(stream_ptr)));
+    HIP_TRY(launch_clip_flag(x, n, flag, c->sync_ws(), static_cast<hipStream_t>(stream_ptr)));
     return MPCD_OK;
 }
 
@@ -734,7 +748,7 @@ int mpcd_rollout_cost(mpcd_ctx *c, const mpcd_system_desc *sys, const double *x0
     HIP_TRY(hipSetDevice(c->device));
     const int *flag = clip_flag;
     if (!flag) {
-        HIP_TRY(launch_clip_flag(u_norm, batch * horizon * sys->n_u, c->flag.as<int>(), st));
+        HIP_TRY(launch_clip_flag(u_norm, batch * horizon * sys->n_u, c->flag.as<int>(), c->sync_ws(), st));
         flag = c->flag.as<int>();
     }
     HIP_TRY(launch_rollout_cost(*sys, x0, nullptr, batch, u_norm, umin, umax, flag, batch, horizon, cost, st));
@@ -812,7 +826,7 @@ int mpcd_unnormalize(mpcd_ctx *c, const float *x, int64_t n_rows, int32_t dim, c
     HIP_TRY(hipSetDevice(c->device));
     const int *flag = clip_flag;
     if (!flag) {
-        HIP_TRY(launch_clip_flag(x, n_rows * dim, c->flag.as<int>(), st));
+        HIP_TRY(launch_clip_flag(x, n_rows * dim, c->flag.as<int>(), c->sync_ws(), st));
         flag = c->flag.as<int>();
     }
     HIP_TRY(launch_unnormalize(x, n_rows * dim, dim, flag, mn, mx, out, st));
@@ -918,6 +932,89 @@ int mpcd_select(mpcd_ctx *c, const double *cost_local, int64_t n_local, const fl
     HIP_TRY(launch_argmin(costs_all, n_local * c->nranks, 0, best_dev, st));
     HIP_TRY(launch_winner_row(best_dev, (int64_t)c->rank * n_local, n_local, rows_local, row_len, row_out, st));
     if (c->comm) NCCL_TRY(ncclAllReduce(row_out, row_out, (size_t)row_len, ncclFloat32, ncclSum, c->comm, st));
+    return MPCD_OK;
+}
+
+int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, float *u_best_host, void *stream)
+{
+    if (!c || !a || !a->sys || !a->x0 || !a->act_min || !a->act_max || !a->cost_local || !best_host || !u_best_host)
+        return fail(MPCD_EINVAL, "null argument");
+    if (!c->net_loaded) return fail(MPCD_ESTATE, "no net loaded");
+    const mpcd_net_desc &d = c->desc;
+    const mpcd_system_desc &sys = *a->sys;
+    const int64_t B = a->sample.batch;
+    const int H = d.horizon, row = H * d.state_dim;
+    if (B < 1 || !a->sample.x_out) return fail(MPCD_EINVAL, "sample.batch / sample.x_out");
+    if (sys.n_u != d.state_dim) return fail(MPCD_EINVAL, "system n_u %d != net state_dim %d", sys.n_u, d.state_dim);
+    int rc = check_system(&sys, H);
+    if (rc) return rc;
+    if (d.context_dim > 0 && (!a->ctx_min || !a->ctx_max)) return fail(MPCD_EINVAL, "ctx_min / ctx_max");
+    if (d.context_dim > 0 && d.context_dim != sys.n_x) return fail(MPCD_EINVAL, "context_dim %d != n_x %d", d.context_dim, sys.n_x);
+    if (c->comm && !a->costs_all) return fail(MPCD_EINVAL, "costs_all is required with a communicator");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipSetDevice(c->device));
+
+    // host staging (pinned): [context row | result block]
+    const size_t out_bytes = sizeof(mpcd_best) + sizeof(float) * (size_t)row;
+    const size_t host_bytes = 64 + out_bytes;
+    if (c->step_host_bytes < host_bytes) {
+        if (c->step_host) (void)hipHostFree(c->step_host);
+        c->step_host = nullptr;
+        c->step_host_bytes = 0;
+        HIP_TRY(hipHostMalloc(&c->step_host, host_bytes, hipHostMallocDefault));
+        c->step_host_bytes = host_bytes;
+    }
+    if ((rc = c->step_ctx.ensure(64)) || (rc = c->step_out.ensure(out_bytes))) return rc;
+    const int64_t n_part = (B + kRolloutBlock - 1) / kRolloutBlock;
+    if ((rc = c->step_part.ensure(16 * (size_t)n_part + sizeof(float) * (size_t)row))) return rc;
+
+    // normalize_condition (A12), fp64 then the net's .float()
+    mpcd_sample_args sa = a->sample;
+    if (d.context_dim > 0) {
+        float *ch = static_cast<float *>(c->step_host);
+        for (int i = 0; i < d.context_dim; ++i) {
+            const double den = (double)(a->ctx_max[i] - a->ctx_min[i]);
+            ch[i] = (float)(2.0 * ((a->x0[i] - (double)a->ctx_min[i]) / den) - 1.0);
+        }
+        HIP_TRY(hipMemcpyAsync(c->step_ctx.p, ch, sizeof(float) * d.context_dim, hipMemcpyHostToDevice, st));
+        sa.context = c->step_ctx.as<float>();
+        sa.context_shared = 1;
+    } else {
+        sa.context = nullptr;
+    }
+    if ((rc = mpcd_sample(c, &sa, stream))) return rc;
+
+    // LimitsNormalizer's global clip flag: provably 0, this rank's own, or the OR over ranks
+    int *flags = c->flag.as<int>();
+    const int *flag = flags + 1;  // flag[1] is never written: a constant 0
+    if (!a->flag_zero) {
+        HIP_TRY(launch_clip_flag(sa.x_out, B * row, flags, c->sync_ws(), st));
+        if (c->comm) NCCL_TRY(ncclAllReduce(flags, flags, 1, ncclInt32, ncclMax, c->comm, st));
+        flag = flags;
+    }
+    mpcd_best *best_dev = c->step_out.as<mpcd_best>();
+    float *u_dev = reinterpret_cast<float *>(best_dev + 1);
+    double *part_cost = c->step_part.as<double>();
+    int64_t *part_idx = reinterpret_cast<int64_t *>(part_cost + n_part);
+    if (!c->comm) {  // rollout + cost + argmin + the winner's unnormalised row in one launch
+        RolloutSelect sel{best_dev, u_dev, part_cost, part_idx, c->sync_ws() + 8, n_part, sa.global_offset};
+        HIP_TRY(launch_rollout_cost(sys, a->x0, nullptr, B, sa.x_out, a->act_min, a->act_max, flag, B, H,
+                                    a->cost_local, st, &sel));
+    } else {
+        HIP_TRY(launch_rollout_cost(sys, a->x0, nullptr, B, sa.x_out, a->act_min, a->act_max, flag, B, H,
+                                    a->cost_local, st));
+        float *row_norm = reinterpret_cast<float *>(part_idx + n_part);
+        if ((rc = comm_gather(c, a->cost_local, a->costs_all, (size_t)B, ncclFloat64, 8, st))) return rc;
+        HIP_TRY(launch_argmin(a->costs_all, B * c->nranks, 0, best_dev, st));
+        HIP_TRY(launch_winner_row(best_dev, (int64_t)c->rank * B, B, sa.x_out, row, row_norm, st));
+        NCCL_TRY(ncclAllReduce(row_norm, row_norm, (size_t)row, ncclFloat32, ncclSum, c->comm, st));
+        HIP_TRY(launch_unnormalize(row_norm, row, d.state_dim, flag, a->act_min, a->act_max, u_dev, st));
+    }
+    void *host_out = static_cast<char *>(c->step_host) + 64;
+    HIP_TRY(hipMemcpyAsync(host_out, c->step_out.p, out_bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    memcpy(best_host, host_out, sizeof(mpcd_best));
+    memcpy(u_best_host, static_cast<char *>(host_out) + sizeof(mpcd_best), sizeof(float) * (size_t)row);
     return MPCD_OK;
 }
 

@@ -16,7 +16,8 @@
 
 namespace {
 
-constexpr int RT_THREADS = 64;  // candidates per workgroup
+constexpr int RT_THREADS = 64;  // candidates per workgroup (one wave: the fused argmin is a wave reduction)
+static_assert(RT_THREADS == kRolloutBlock, "RolloutSelect partial count");
 
 struct SysK {
     int32_t system, cost_kind, nx, nu;
@@ -29,6 +30,33 @@ struct SysK {
 struct MinMax {
     float mn[16], mx[16];
 };
+
+// Fused selection (single-rank control step): block argmins -> the last block reduces them, writes
+// *best and the winner's unnormalised [H][n_u] row. part_* hold one entry per block; counter is zero
+// between launches (the last block resets it).
+struct SelectK {
+    mpcd_best *best;
+    float *row_out;      // [H * n_u] unnormalised winner row
+    double *part_cost;   // [gridDim.x]
+    int64_t *part_idx;   // [gridDim.x]
+    unsigned *counter;
+    int64_t offset;      // global index of candidate 0
+};
+
+// (v, i) beats (bv, bi): NaN = +inf, lower cost, then lower index; i < 0 = empty
+__device__ __forceinline__ bool better(double v, int64_t i, double bv, int64_t bi)
+{
+    return i >= 0 && (bi < 0 || v < bv || (v == bv && i < bi));
+}
+__device__ __forceinline__ void wave_argmin(double &v, int64_t &i)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const double ov = __shfl_xor(v, m);
+        const int64_t oi = __shfl_xor(i, m);
+        if (better(ov, oi, v, i)) { v = ov; i = oi; }
+    }
+}
 
 // State / input sizes per system: compile-time, so every per-candidate array lives in registers
 // (a runtime n_x indexed them dynamically and put them in scratch memory).
@@ -124,16 +152,33 @@ __device__ __forceinline__ void dyn_step(const SysK &S, const double *x, const d
     }
 }
 
-// any |u_norm| outside [-1-eps, 1+eps]  ->  *flag = 1   (x.max() > 1+eps or x.min() < -1-eps)
-__global__ void clip_flag_kernel(const float *x, int64_t n, int *flag)
+// any |u_norm| outside [-1-eps, 1+eps]  ->  *flag = 1, else 0  (x.max() > 1+eps or x.min() < -1-eps).
+// One launch, no memset: blocks OR into ws[0]; the last block to finish (ws[1] counts them) moves the
+// result to *flag and leaves ws zeroed for the next launch on the stream.
+__global__ __launch_bounds__(256) void clip_flag_kernel(const float *x, int64_t n, int *flag, unsigned *ws)
 {
     const float hi = (float)(1.0 + 1e-4), lo = (float)(-1.0 - 1e-4);
     int any = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n4 = ((uintptr_t)x & 15) ? 0 : n >> 2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const f32x4 v = reinterpret_cast<const f32x4 *>(x)[i];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) any |= (v[e] > hi) | (v[e] < lo);
+    }
+    for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const float v = x[i];
         any |= (v > hi) | (v < lo);
     }
-    if (__any(any) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+    any = __syncthreads_or(any);
+    if (threadIdx.x == 0) {
+        if (any) atomicOr(ws, 1u);
+        __threadfence();
+        if (atomicAdd(ws + 1, 1u) == gridDim.x - 1) {
+            __threadfence();
+            *flag = (int)atomicExch(ws, 0u);
+            atomicExch(ws + 1, 0u);
+        }
+    }
 }
 
 __device__ __forceinline__ float unnorm1(float v, bool clip, float mn, float mx)
@@ -155,10 +200,11 @@ __global__ void unnormalize_kernel(const float *x, int64_t n, int dim, const int
 // x0_dev == nullptr: every candidate starts from S.x0; else candidate b starts from x0_dev[b / group]
 // (closed loop: one plant state per group of candidates). flags[b / group] is that group's clip flag
 // (group = batch for the single-state case: one global flag).
-template <int SYS>
+// SEL: also select (SelectK above) - one launch for rollout, cost, argmin and the winner's row.
+template <int SYS, bool SEL>
 __global__ __launch_bounds__(RT_THREADS) void rollout_cost_kernel(const SysK S, const float *u_norm, const int *flags,
                                                                   const double *x0_dev, int64_t group, int64_t batch,
-                                                                  int H, double *cost)
+                                                                  int H, double *cost, const SelectK K)
 {
     constexpr int nx = SysDim<SYS>::NX, nu = SysDim<SYS>::NU;
     extern __shared__ float su[];  // [RT_THREADS][H*nu + 1]
@@ -166,18 +212,26 @@ __global__ __launch_bounds__(RT_THREADS) void rollout_cost_kernel(const SysK S, 
     const int64_t c0 = (int64_t)blockIdx.x * RT_THREADS;
     const int64_t nvalid = min((int64_t)RT_THREADS, batch - c0);
     const float *src = u_norm + (size_t)c0 * row;
-    for (int i = threadIdx.x; i < nvalid * row; i += RT_THREADS) {
-        const int c = i / row, k = i - c * row;
-        su[c * stride + k] = src[i];
+    if ((row & 3) == 0) {  // 16-byte loads (a row never straddles a quad)
+        for (int i = threadIdx.x; i < nvalid * row / 4; i += RT_THREADS) {
+            const f32x4 v = ldg4(src + 4 * i);
+            const int c = 4 * i / row, k = 4 * i - c * row;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) su[c * stride + k + e] = v[e];
+        }
+    } else {
+        for (int i = threadIdx.x; i < nvalid * row; i += RT_THREADS) {
+            const int c = i / row, k = i - c * row;
+            su[c * stride + k] = src[i];
+        }
     }
     __syncthreads();
-    const int64_t b = c0 + threadIdx.x;
-    if (b >= batch) return;
+    const int64_t b = min(c0 + threadIdx.x, batch - 1);  // lanes past the batch recompute the last one
     const bool clip = flags[b / group] != 0;
     float mn[nu], mx[nu];
 #pragma unroll
     for (int i = 0; i < nu; ++i) { mn[i] = S.umin[i]; mx[i] = S.umax[i]; }
-    const float *ur = su + threadIdx.x * stride;
+    const float *ur = su + (b - c0) * stride;
     double x[nx], xn[nx], u[nu];
 #pragma unroll
     for (int i = 0; i < nx; ++i) x[i] = x0_dev ? x0_dev[(b / group) * nx + i] : S.x0[i];
@@ -211,7 +265,40 @@ __global__ __launch_bounds__(RT_THREADS) void rollout_cost_kernel(const SysK S, 
             for (int j = 0; j < nx; ++j) x[j] = xn[j];
         }
     }
-    cost[b] = J;
+    if (c0 + threadIdx.x < batch) cost[b] = J;
+    if constexpr (SEL) {
+        double v = isnan(J) ? INFINITY : J;
+        int64_t i = c0 + threadIdx.x < batch ? b : -1;
+        wave_argmin(v, i);  // RT_THREADS == one wave
+        __shared__ bool last;
+        if (threadIdx.x == 0) {
+            K.part_cost[blockIdx.x] = v;
+            K.part_idx[blockIdx.x] = i;
+            __threadfence();
+            last = atomicAdd(K.counter, 1u) == gridDim.x - 1;
+        }
+        __syncthreads();
+        if (!last) return;
+        __threadfence();
+        v = INFINITY;
+        i = -1;
+        for (int k = threadIdx.x; k < (int)gridDim.x; k += RT_THREADS) {
+            const double pv = __builtin_nontemporal_load(K.part_cost + k);
+            const int64_t pi = __builtin_nontemporal_load(K.part_idx + k);
+            if (better(pv, pi, v, i)) { v = pv; i = pi; }
+        }
+        wave_argmin(v, i);
+        if (threadIdx.x == 0) {
+            K.best->cost = v;
+            K.best->index = i < 0 ? -1 : K.offset + i;
+            *K.counter = 0u;
+        }
+        if (i >= 0 && K.row_out) {
+            const bool clip0 = flags[0] != 0;
+            for (int k = threadIdx.x; k < row; k += RT_THREADS)
+                K.row_out[k] = unnorm1(u_norm[(size_t)i * row + k], clip0, S.umin[k % nu], S.umax[k % nu]);
+        }
+    }
 }
 
 // Per-group clip flags: flags[g] = any element of x[g*group_elems, (g+1)*group_elems) outside
@@ -362,12 +449,11 @@ hipError_t launch_winner_row(const mpcd_best *best, int64_t lo, int64_t n_local,
     return hipGetLastError();
 }
 
-hipError_t launch_clip_flag(const float *x, int64_t n, int *flag_dev, hipStream_t stream)
+hipError_t launch_clip_flag(const float *x, int64_t n, int *flag_dev, unsigned *ws, hipStream_t stream)
 {
-    hipError_t e = hipMemsetAsync(flag_dev, 0, sizeof(int), stream);
-    if (e != hipSuccess) return e;
-    const int64_t blocks = std::min<int64_t>(1024, (n + 255) / 256);
-    hipLaunchKernelGGL(clip_flag_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, stream, x, n, flag_dev);
+    const int64_t blocks = std::min<int64_t>(512, (n + 1023) / 1024);
+    hipLaunchKernelGGL(clip_flag_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, stream, x, n, flag_dev,
+                       ws);
     return hipGetLastError();
 }
 
@@ -387,7 +473,7 @@ hipError_t launch_unnormalize(const float *x, int64_t n, int dim, const int *fla
 
 hipError_t launch_rollout_cost(const mpcd_system_desc &d, const double *x0_host, const double *x0_dev, int64_t group,
                                const float *u_norm, const float *umin_host, const float *umax_host, const int *flag_dev,
-                               int64_t batch, int H, double *cost, hipStream_t stream)
+                               int64_t batch, int H, double *cost, hipStream_t stream, const RolloutSelect *sel)
 {
     if (group < 1) group = batch;
     SysK S = {};
@@ -401,12 +487,21 @@ hipError_t launch_rollout_cost(const mpcd_system_desc &d, const double *x0_host,
     for (int i = 0; i < d.n_x; ++i) S.x0[i] = x0_host ? x0_host[i] : 0.0;
     for (int i = 0; i < d.n_u; ++i) { S.umin[i] = umin_host[i]; S.umax[i] = umax_host[i]; }
     const size_t lds = sizeof(float) * RT_THREADS * (H * d.n_u + 1);
+    SelectK K = {};
+    if (sel) {
+        if (group != batch || sel->n_part < (batch + RT_THREADS - 1) / RT_THREADS) return hipErrorInvalidValue;
+        K = SelectK{sel->best, sel->row_out, sel->part_cost, sel->part_idx, sel->counter, sel->offset};
+    }
     const dim3 grid((unsigned)((batch + RT_THREADS - 1) / RT_THREADS));
 #define MPCD_ROLLOUT(SYS_)                                                                                          \
     case SYS_:                                                                                                      \
         if (d.n_x != SysDim<SYS_>::NX || d.n_u != SysDim<SYS_>::NU) return hipErrorInvalidValue;                    \
-        hipLaunchKernelGGL(rollout_cost_kernel<SYS_>, grid, dim3(RT_THREADS), lds, stream, S, u_norm, flag_dev, x0_dev, \
-                           group, batch, H, cost);                                                                  \
+        if (sel)                                                                                                    \
+            hipLaunchKernelGGL((rollout_cost_kernel<SYS_, true>), grid, dim3(RT_THREADS), lds, stream, S, u_norm,   \
+                               flag_dev, x0_dev, group, batch, H, cost, K);                                         \
+        else                                                                                                        \
+            hipLaunchKernelGGL((rollout_cost_kernel<SYS_, false>), grid, dim3(RT_THREADS), lds, stream, S, u_norm,  \
+                               flag_dev, x0_dev, group, batch, H, cost, K);                                         \
         break;
     switch (d.system) {
         MPCD_ROLLOUT(MPCD_SYS_CARTPOLE_LIN5)

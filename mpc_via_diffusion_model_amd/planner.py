@@ -26,6 +26,7 @@ from . import distributed as D
 from . import schedule as S
 from .systems import System
 
+_STEP_CONTEXT = object()  # _args placeholder: mpcd_mpc_step normalises x0 into the context itself
 _SAMPLERS = {"ddpm_cfg": N.MPCD_DDPM_CFG, "ddpm_cart_pole_sample_fn": N.MPCD_DDPM_CFG,
              "ddim_cfg": N.MPCD_DDIM_CFG, "ddim": N.MPCD_DDIM, "ddim_sample": N.MPCD_DDIM}
 
@@ -95,8 +96,8 @@ class DiffusionMPC:
                                                                         np.ones(spec.context_dim))
         a_lo, a_hi = action_limits if action_limits is not None else (-np.ones(spec.state_dim),
                                                                       np.ones(spec.state_dim))
-        self.ctx_min = np.asarray(c_lo, dtype=np.float32)
-        self.ctx_max = np.asarray(c_hi, dtype=np.float32)
+        self.ctx_min = np.ascontiguousarray(c_lo, dtype=np.float32)
+        self.ctx_max = np.ascontiguousarray(c_hi, dtype=np.float32)
         self.act_min = np.ascontiguousarray(a_lo, dtype=np.float32)
         self.act_max = np.ascontiguousarray(a_hi, dtype=np.float32)
         self._lib = N.lib()
@@ -177,7 +178,7 @@ class DiffusionMPC:
     def _args(self, sampler, batch, context, w, n_wo_noise, ddim_steps, clamp_x0, seed, global_offset, noise,
               x_out, chain):
         a = N.SampleArgs()
-        if self.spec.context_dim > 0:
+        if self.spec.context_dim > 0 and context is not _STEP_CONTEXT:
             if context is None:
                 raise ValueError("this net needs a context")
             a.context = context.data_ptr()
@@ -356,12 +357,22 @@ class DiffusionMPC:
                                 cost=cs.t().cpu().numpy(), index=ix.t().cpu().numpy())
 
     def mpc_step(self, x0, system: System, n_samples, w=0.01, sample_fn="ddpm_cfg", n_wo_noise=0, ddim_steps=None,
-                 clamp_x0=False, seed=0, noise=None, group=None, comm=None):
+                 clamp_x0=False, seed=0, noise=None, group=None, comm=None, native=None):
         """One control step: sample n_samples candidates on this rank (weak scaling: every rank adds
         n_samples), roll out + cost them, all-gather costs, pick the global argmin, broadcast it.
         comm: a distributed.NativeComm (the exchange inside libmpcd.so over RCCL) or None
-        (torch.distributed collectives on `group`)."""
+        (torch.distributed collectives on `group`).
+        native: run the whole step as one mpcd_mpc_step call (default whenever the library can do the
+        exchange itself: a NativeComm, or a single rank); False = the step composed from the separate
+        entry points (sample, clip flag, rollout, select), kept as the reference composition."""
         rank, size = D.world(group)
+        if native is None:
+            native = comm is not None or size == 1
+        if native:
+            if size > 1 and comm is None:
+                raise ValueError("native mpc_step on several ranks needs a NativeComm")
+            return self._mpc_step_native(x0, system, n_samples, w, sample_fn, n_wo_noise, ddim_steps, clamp_x0, seed,
+                                         noise, comm)
         offset, total = D.shard(n_samples, group)
         ctx = torch.from_numpy(self.normalize_condition(x0)[None])
         u_norm = self.sample_trajectories(ctx, n_samples, self.spec.horizon, w, sample_fn, n_wo_noise, ddim_steps,
@@ -383,4 +394,40 @@ class DiffusionMPC:
         u_best = self.unnormalize_states(row[None], flag)[0]
         u_host = u_best.cpu().numpy()
         return MPCResult(u0=u_host[0].copy(), u_best=u_host, best_cost=best, best_index=idx, costs=costs,
+                         u_norm=u_norm)
+
+    def _mpc_step_native(self, x0, system, n_samples, w, sample_fn, n_wo_noise, ddim_steps, clamp_x0, seed, noise,
+                         comm):
+        """mpc_step as one libmpcd call (mpcd_mpc_step): one H2D copy of the context row, the kernels,
+        one D2H copy of {best, u_best}, one stream synchronisation."""
+        size, rank = (comm.size, comm.rank) if comm is not None else (1, 0)
+        B, H, d = int(n_samples), self.spec.horizon, self.spec.state_dim
+        if d != system.n_u:
+            raise ValueError(f"system {system.name} has {system.n_u} inputs, samples have {d}")
+        sampler = self._sampler_id(sample_fn)
+        steps = self.n_denoise_steps(sample_fn, n_wo_noise, ddim_steps)
+        if noise is not None:
+            noise = noise.to(self.device, torch.float32).contiguous()
+            if tuple(noise.shape) != (steps + 1, B, H, d):
+                raise ValueError(f"noise must be [{steps + 1}, {B}, {H}, {d}], got {tuple(noise.shape)}")
+        u_norm = torch.empty((B, H, d), dtype=torch.float32, device=self.device)
+        cost = torch.empty(B, dtype=torch.float64, device=self.device)
+        costs = torch.empty(size * B, dtype=torch.float64, device=self.device) if size > 1 else cost
+        x0 = np.ascontiguousarray(x0, dtype=np.float64)
+        desc = system.desc()
+        a = N.StepArgs()
+        a.sys = ctypes.pointer(desc)
+        a.x0 = x0.ctypes.data
+        a.ctx_min, a.ctx_max = self.ctx_min.ctypes.data, self.ctx_max.ctypes.data
+        a.act_min, a.act_max = self.act_min.ctypes.data, self.act_max.ctypes.data
+        a.sample = self._args(sampler, B, _STEP_CONTEXT, w, n_wo_noise, ddim_steps, clamp_x0, seed, rank * B, noise,
+                              u_norm, None)
+        a.flag_zero = 1 if (sampler == N.MPCD_DDPM_CFG and self.ddpm_final_in_range) else 0
+        a.cost_local = cost.data_ptr()
+        a.costs_all = costs.data_ptr()
+        best = N.Best()
+        u_best = np.empty((H, d), dtype=np.float32)
+        N.check(self._lib.mpcd_mpc_step(self._ctx, ctypes.byref(a), ctypes.byref(best), u_best.ctypes.data,
+                                        self._stream()), "mpcd_mpc_step")
+        return MPCResult(u0=u_best[0].copy(), u_best=u_best, best_cost=best.cost, best_index=best.index, costs=costs,
                          u_norm=u_norm)

@@ -43,11 +43,13 @@ def test_native_select_matches_torch_exchange(rccl):
     comm = D.NativeComm(plan)
     sysm = systems.double_int2d()
     x0 = np.array([0.3, -0.2, 0.1, 0.05])
-    a = plan.mpc_step(x0, sysm, 512, seed=11)
-    b = plan.mpc_step(x0, sysm, 512, seed=11, comm=comm)
-    assert (a.best_index, a.best_cost) == (b.best_index, b.best_cost)
-    np.testing.assert_array_equal(a.u_best, b.u_best)
-    assert torch.equal(a.costs, b.costs)
+    a = plan.mpc_step(x0, sysm, 512, seed=11, native=False)           # torch exchange, composed step
+    b = plan.mpc_step(x0, sysm, 512, seed=11, comm=comm, native=False)  # mpcd_select, composed step
+    c = plan.mpc_step(x0, sysm, 512, seed=11, comm=comm)                # mpcd_mpc_step (RCCL branch if rccl)
+    for r in (b, c):
+        assert (a.best_index, a.best_cost) == (r.best_index, r.best_cost)
+        np.testing.assert_array_equal(a.u_best, r.u_best)
+        assert torch.equal(a.costs, r.costs)
 
 
 def test_native_select_nan_and_ties():

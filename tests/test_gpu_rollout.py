@@ -92,9 +92,12 @@ def test_argmin_nan_and_ties():
     assert plan.argmin(big.cuda()) == (77777, 0.5)
 
 
-def test_mpc_step_matches_oracle_pipeline():
-    """normalise -> CFG-DDPM sample -> unnormalise -> rollout/cost -> argmin, vs the oracle."""
-    d, H, C, N, B = 1, 32, 5, 25, 128
+@pytest.mark.parametrize("native", [False, True])
+@pytest.mark.parametrize("B", [128, 100])
+def test_mpc_step_matches_oracle_pipeline(native, B):
+    """normalise -> CFG-DDPM sample -> unnormalise -> rollout/cost -> argmin, vs the oracle; native =
+    the one-call mpcd_mpc_step (fused rollout + argmin + winner row), else the composed entry points."""
+    d, H, C, N = 1, 32, 5, 25
     net = make_mlp(d, H, C, seed=9)
     lo, hi = np.array([-20.0]), np.array([20.0])
     cmin = np.array([-5, -5, 2, -5, 0], dtype=np.float32)
@@ -104,7 +107,7 @@ def test_mpc_step_matches_oracle_pipeline():
     red = lambda th: (th - np.pi) ** 2 / -np.pi + np.pi  # noqa: E731
     x0 = np.array([0.3, 0.1, 0.95 * np.pi, -0.2, red(0.95 * np.pi)])
     noise = torch.randn(N + 1, B, H, d, generator=torch.Generator().manual_seed(1))
-    res = plan.mpc_step(x0, systems.cartpole_lin5(), B, w=0.01, noise=noise)
+    res = plan.mpc_step(x0, systems.cartpole_lin5(), B, w=0.01, noise=noise, native=native)
     # oracle pipeline
     from oracle import normalizer as onorm
     ctx = onorm.normalize(torch.from_numpy(x0)[None], torch.from_numpy(cmin), torch.from_numpy(cmax)).float()
@@ -118,3 +121,38 @@ def test_mpc_step_matches_oracle_pipeline():
         assert abs(cost[res.best_index] - cost[i]) <= 1e-4 * abs(cost[i])
     np.testing.assert_allclose(res.u_best, u[res.best_index].numpy(), rtol=1e-4, atol=1e-4 * 20)
     assert res.u0.shape == (d,)
+
+
+@pytest.mark.parametrize("B", [64, 1000, 4096 + 17])
+@pytest.mark.parametrize("sample_fn", ["ddpm_cfg", "ddim_cfg"])
+def test_native_step_equals_composed_step(B, sample_fn):
+    """mpcd_mpc_step (one call, fused select) gives bit-identical samples, costs, winner and trajectory
+    to the step composed from sample / clip flag / rollout / argmin / unnormalise; ragged B included
+    (the last rollout workgroup is partial). DDIM leaves the clip flag live (no provable bound)."""
+    d, H, C = 2, 32, 4
+    net = make_mlp(d, H, C, seed=5)
+    plan = DiffusionMPC(NetSpec("mlp", d, H, C), net.state_dict(), n_diffusion_steps=25,
+                        action_limits=(np.array([-2.0, -0.5]), np.array([2.0, 0.5])))
+    x0 = np.array([0.4, -0.3, 0.2, -0.1])
+    sysm = systems.double_int2d()
+    a = plan.mpc_step(x0, sysm, B, sample_fn=sample_fn, seed=7, native=False)
+    b = plan.mpc_step(x0, sysm, B, sample_fn=sample_fn, seed=7, native=True)
+    assert torch.equal(a.u_norm, b.u_norm)
+    assert torch.equal(a.costs, b.costs)
+    assert (a.best_index, a.best_cost) == (b.best_index, b.best_cost)
+    np.testing.assert_array_equal(a.u_best, b.u_best)
+    np.testing.assert_array_equal(a.u0, b.u0)
+
+
+def test_native_step_ties_pick_lowest_index():
+    """Every candidate gets the same injected noise -> identical trajectories and costs: the fused
+    argmin must return index 0 (lowest index on ties), across several rollout workgroups."""
+    d, H, C, N, B = 1, 32, 5, 25, 300
+    net = make_mlp(d, H, C, seed=2)
+    plan = DiffusionMPC(NetSpec("mlp", d, H, C), net.state_dict(), n_diffusion_steps=N)
+    noise = torch.randn(N + 1, 1, H, d, generator=torch.Generator().manual_seed(3)).expand(N + 1, B, H, d)
+    x0 = np.array([0.1, 0.0, 0.2, 0.0, 0.3])
+    res = plan.mpc_step(x0, systems.cartpole_lin5(), B, noise=noise, native=True)
+    c = res.costs.cpu()
+    assert torch.all(c == c[0])
+    assert res.best_index == 0 and res.best_cost == float(c[0])

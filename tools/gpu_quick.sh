@@ -1,10 +1,7 @@
-# quick loop: GPU tests, layer profile (prof build, if built), bench (f32x3 and f32)
+# Quick GPU pass: the rollout / comm / MLP parity tests, then the default bench (no CPU baseline).
 cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 400 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log; if [ $rc -gt 1 ]; then exit $rc; fi
-if [ -f mpc_via_diffusion_model_amd/libmpcd_prof.so ]; then
-  MPCD_LIB=mpc_via_diffusion_model_amd/libmpcd_prof.so DTYPE=f32x3 timeout -k 10 200 python tools/layer_prof.py > gpurun_out/layer_prof.log 2>&1 || exit $?
-fi
-timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --dtype f32x3 > gpurun_out/bench.log 2>&1 || exit $?
-timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --dtype f32 > gpurun_out/bench_f32.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_rollout.py tests/test_gpu_comm.py tests/test_gpu_closed_loop.py -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_quick.log 2>&1 || exit $?
+timeout -k 10 200 python bench.py --no-cpu-baseline > gpurun_out/bench_quick.log 2>&1 || exit $?
+timeout -k 10 200 python bench.py --no-cpu-baseline --steps 40 --warmup 10 >> gpurun_out/bench_quick.log 2>&1 || exit $?
