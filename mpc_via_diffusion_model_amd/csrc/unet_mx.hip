@@ -21,9 +21,14 @@
 // through LDS (reusing the staged input when one job per wave suffices) for the GroupNorm statistics
 // (fp64, shifted) and the elementwise epilogue, stored coalesced channels-last.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
 #include <string>
 
 #include "unet.h"
@@ -423,6 +428,53 @@ hipError_t launch_kind(const ConvMK &k, Tile t, size_t lds, hipStream_t st)
     return hipErrorInvalidValue;
 }
 
+struct MxChoice {
+    int rb;
+    Tile t;
+    int alias;
+    size_t lds;
+    int stat_off;  // LDS byte offset of the GroupNorm statistics
+    double model;  // issue-model cost per row (ranks the candidates)
+};
+
+struct MxKey {
+    int kind, planes, ca, cb, cout, lin, lout, epi;
+    int64_t rows, x_rows;
+    bool operator<(const MxKey &o) const
+    {
+        return std::tie(kind, planes, ca, cb, cout, lin, lout, epi, rows, x_rows) <
+               std::tie(o.kind, o.planes, o.ca, o.cb, o.cout, o.lin, o.lout, o.epi, o.rows, o.x_rows);
+    }
+};
+std::mutex g_mx_mu;
+std::map<MxKey, MxChoice> g_mx_cache;  // measured pick per layer shape and batch (process-wide)
+
+bool autotune_on()
+{
+    static const bool on = [] {
+        const char *e = getenv("MPCD_UNET_AUTOTUNE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+hipError_t launch_choice(int kind, int planes, ConvMK &k, const MxChoice &ch, hipStream_t st)
+{
+    k.rb = ch.rb;
+    k.alias = ch.alias;
+    k.stat_off = ch.stat_off;
+#define K_(KD)                                                                        \
+    if (kind == KD)                                                                   \
+        return planes == 1 ? launch_kind<KD, 1>(k, ch.t, ch.lds, st)                  \
+                           : launch_kind<KD, 3>(k, ch.t, ch.lds, st);
+    K_(UCONV_SAME5)
+    K_(UCONV_DOWN3)
+    K_(UCONV_UP4)
+    K_(UCONV_PW1)
+#undef K_
+    return hipErrorInvalidValue;
+}
+
 }  // namespace
 
 void unet_pack_mx(int kind, int cin, int cout, int planes, const float *w_host, ConvLayer &L,
@@ -490,56 +542,6 @@ hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::
     int cs = cinp * 2;
     if (((cs / 16) & 1) == 0) cs += 16;
     k.cs = cs;
-    const int win = k.lin + k.halo_l + k.halo_r;
-    const int NT = k.coutp / 16, npar = kind == UCONV_UP4 ? 2 : 1;
-    const int nprod = planes == 1 ? 1 : 6;
-    const Tile *tiles = planes == 1 ? kTiles1 : kTiles3;
-    const int ntiles = planes == 1 ? 5 : 3;
-    const size_t cap = 160 * 1024;
-    double best = 1e30;
-    int best_rb = 0, best_alias = 0;
-    Tile best_t{1, 4};
-    size_t best_lds = 0;
-    for (int rb = 32; rb >= 1; rb /= 2) {
-        if (rb > 1 && (int64_t)rb > k.rows) continue;
-        const int nval = kind == UCONV_UP4 ? rb * k.lin : rb * k.lout;
-        const int ctp = (nval + 15) / 16;
-        const size_t in_b = (size_t)planes * rb * win * cs;
-        const size_t out_b = (size_t)npar * ctp * 16 * (k.coutp + 4) * 4;
-        const size_t stat_b = (size_t)(2 * rb * 32 + 4) * 4 + (size_t)4 * k.coutp * 4;
-        for (int ti = 0; ti < ntiles; ++ti) {
-            const Tile t = tiles[ti];
-            const int jobs = ((NT + t.nn - 1) / t.nn) * ((ctp + t.nc - 1) / t.nc) * npar;
-            const int alias = jobs <= MT / 64;
-            const size_t lds = (alias ? std::max(in_b, out_b) : in_b + out_b) + stat_b;
-            if (lds > cap) continue;
-            // per-row cost: MFMA tile slots of the busiest wave (padding included) + fragment loads
-            const int per_wave = (jobs + 3) / 4;
-            const double cyc = (double)per_wave * KC *
-                                   (t.nn * t.nc * nprod * 16.0 + t.nn * planes * 24.0 + t.nc * planes * 8.0) +
-                               (double)in_b / 64.0 + 600.0;
-            const double cost = cyc / rb;
-            if (cost < best * 0.999) {
-                best = cost;
-                best_rb = rb;
-                best_t = t;
-                best_alias = alias;
-                best_lds = lds;
-            }
-        }
-    }
-    if (!best_rb) {
-        if (why) *why = "UNet mx conv: no tiling fits LDS";
-        return hipErrorInvalidValue;
-    }
-    k.rb = best_rb;
-    k.alias = best_alias;
-    {
-        const int nval = kind == UCONV_UP4 ? best_rb * k.lin : best_rb * k.lout;
-        const size_t in_b = (size_t)planes * best_rb * win * cs;
-        const size_t out_b = (size_t)npar * ((nval + 15) / 16) * 16 * (k.coutp + 4) * 4;
-        k.stat_off = (int)(best_alias ? std::max(in_b, out_b) : in_b + out_b);
-    }
     if (k.epi != UEPI_BIAS) {
         const int cpg = k.cout / k.groups;
         int sh = 0;
@@ -550,14 +552,89 @@ hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::
         }
         k.cpg_shift = sh;
     }
-#define K_(KD)                                                                            \
-    if (kind == KD)                                                                       \
-        return planes == 1 ? launch_kind<KD, 1>(k, best_t, best_lds, st)                  \
-                           : launch_kind<KD, 3>(k, best_t, best_lds, st);
-    K_(UCONV_SAME5)
-    K_(UCONV_DOWN3)
-    K_(UCONV_UP4)
-    K_(UCONV_PW1)
-#undef K_
-    return hipErrorInvalidValue;
+    const int win = k.lin + k.halo_l + k.halo_r;
+    const int NT = k.coutp / 16, npar = kind == UCONV_UP4 ? 2 : 1;
+    const int nprod = planes == 1 ? 1 : 6;
+    const Tile *tiles = planes == 1 ? kTiles1 : kTiles3;
+    const int ntiles = planes == 1 ? 5 : 3;
+    static const size_t cap = [] {  // experiment knob: LDS bytes per workgroup (160 KiB = one per CU)
+        const char *e = getenv("MPCD_UNET_LDS_CAP");
+        return e ? (size_t)atol(e) : (size_t)160 * 1024;
+    }();
+    // Candidates: for each rows-per-workgroup rb, the tile an issue model likes best (MFMA slots of
+    // the busiest wave, padding included, + fragment loads + staging). The model does not see
+    // occupancy - the LDS of a workgroup decides how many share a CU and hide each other's staging
+    // and epilogue latency - so the final pick among the candidates is measured once per layer
+    // shape and batch (autotune below), unless MPCD_UNET_AUTOTUNE=0.
+    std::vector<MxChoice> cands;
+    for (int rb = 32; rb >= 1; rb /= 2) {
+        if (rb > 1 && (int64_t)rb > k.rows) continue;
+        const int nval = kind == UCONV_UP4 ? rb * k.lin : rb * k.lout;
+        const int ctp = (nval + 15) / 16;
+        const size_t in_b = (size_t)planes * rb * win * cs;
+        const size_t out_b = (size_t)npar * ctp * 16 * (k.coutp + 4) * 4;
+        const size_t stat_b = (size_t)(2 * rb * 32 + 4) * 4 + (size_t)4 * k.coutp * 4;
+        MxChoice best{};
+        for (int ti = 0; ti < ntiles; ++ti) {
+            const Tile t = tiles[ti];
+            const int jobs = ((NT + t.nn - 1) / t.nn) * ((ctp + t.nc - 1) / t.nc) * npar;
+            const int alias = jobs <= MT / 64;
+            const size_t body = alias ? std::max(in_b, out_b) : in_b + out_b;
+            const size_t lds = body + stat_b;
+            if (lds > cap) continue;
+            const int per_wave = (jobs + 3) / 4;
+            const double cyc = (double)per_wave * KC *
+                                   (t.nn * t.nc * nprod * 16.0 + t.nn * planes * 24.0 + t.nc * planes * 8.0) +
+                               (double)in_b / 64.0 + 600.0;
+            const double cost = cyc / rb;
+            if (!best.rb || cost < best.model * 0.999) best = MxChoice{rb, t, alias, lds, (int)body, cost};
+        }
+        if (best.rb) cands.push_back(best);
+    }
+    if (cands.empty()) {
+        if (why) *why = "UNet mx conv: no tiling fits LDS";
+        return hipErrorInvalidValue;
+    }
+    std::sort(cands.begin(), cands.end(), [](const MxChoice &x, const MxChoice &y) { return x.model < y.model; });
+
+    const MxKey key{kind, planes, k.ca, k.cb, k.cout, k.lin, k.lout, k.epi, k.rows, k.x_rows};
+    MxChoice pick = cands[0];
+    bool have = false;
+    {
+        std::lock_guard<std::mutex> g(g_mx_mu);
+        auto it = g_mx_cache.find(key);
+        if (it != g_mx_cache.end()) {
+            pick = it->second;
+            have = true;
+        }
+    }
+    // re-running a conv is idempotent unless it writes one of its inputs
+    const bool in_place = k.out == k.xa || (k.xb && k.out == k.xb) || (k.res && k.out == k.res);
+    hipStreamCaptureStatus cap_st = hipStreamCaptureStatusNone;
+    if (!have && cands.size() > 1 && autotune_on() && !in_place && hipStreamIsCapturing(st, &cap_st) == hipSuccess &&
+        cap_st == hipStreamCaptureStatusNone) {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
+            float best_ms = 1e30f;
+            for (const MxChoice &ch : cands) {
+                ConvMK kk = k;
+                if (launch_choice(kind, planes, kk, ch, st) != hipSuccess) continue;  // warm-up (weights into L2)
+                (void)hipEventRecord(e0, st);
+                for (int r = 0; r < 2; ++r) (void)launch_choice(kind, planes, kk, ch, st);
+                (void)hipEventRecord(e1, st);
+                float ms = 0.f;
+                if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) continue;
+                if (ms < best_ms) {
+                    best_ms = ms;
+                    pick = ch;
+                }
+            }
+        }
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        (void)hipGetLastError();
+        std::lock_guard<std::mutex> g(g_mx_mu);
+        g_mx_cache[key] = pick;
+    }
+    return launch_choice(kind, planes, k, pick, st);
 }
