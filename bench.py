@@ -1,14 +1,20 @@
 """Headline benchmark: candidate trajectories denoised + cost-ranked per second.
 
-BASELINE.json metric "candidate trajectories/sec (100 denoise steps, H=32)", workload = configs[1]:
-2D double integrator, 4096 candidates per GPU, H=32, 100 CFG-DDPM steps, MLP noise-net
-(build-defined CFG MLP), fp32. One step = one mpc_step: Philox x_T + 100 CFG
-denoise steps (200 net evaluations) + unnormalise + fp64 rollout/cost + argmin (+ RCCL cost
-all-gather and winner broadcast for N > 1) + the applied action copied to the host.
-Weak scaling: every rank adds 4096 candidates.
+BASELINE.json metric "candidate trajectories/sec (100 denoise steps, H=32)". The default workload is
+configs[1] (cfg2): 2D double integrator, 4096 candidates per GPU, H=32, 100 CFG-DDPM steps, MLP
+noise-net (build-defined CFG MLP), fp32-accurate GEMMs. One step = one mpc_step,
+i.e. one mpcd_mpc_step call: context upload, Philox x_T + the denoising loop (2 net evaluations per
+step) + clip flag + fp64 rollout/cost + argmin + winner row (+ RCCL cost all-gather and winner
+exchange for N > 1) + one D2H copy of the applied trajectory. Weak scaling: every rank adds its
+candidates.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg1..cfg5] [--dtype ...]
   torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+The other BASELINE configs are selectable with --workload (their lines are kept under profiles/):
+cfg1 (the reference's CPU-sized case), cfg3 (pendulum, 1D U-Net, CFG-DDIM 100 steps), cfg4 (cart-pole
+NMPC dynamics, U-Net, H=64; 65536 candidates split over the ranks = strong scaling), cfg5 (12-DoF
+quadrotor, U-Net fp16 operands, 250 steps; 131072 candidates split over the ranks).
 """
 import argparse
 import json
@@ -23,61 +29,92 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-CFG = dict(workload="cfg2: 2D double integrator, MLP noise-net, CFG-DDPM", system="double_int2d", d=2, H=32, C=4,
-           N=100, B=4096, w=0.01, schedule="exponential")
-MAC_FWD = 119552          # MLP MACs per forward at H*d = 64 (incl. time MLP + cond projections)
-MAC_ROW = 95232           # MACs the kernel executes per row and step: the 14 per-row Linears (time MLP and
-                          # cond projections run once per step / per context in the prologues)
+# SURVEY §8d workloads. mac: algorithmic MACs per noise-net forward;
+# mac_row: MACs the kernels execute per row and step on the matrix cores (MLP: the 14 per-row Linears -
+# the time MLP and cond projections run once per step / per context in the prologues).
+WORKLOADS = {
+    "cfg1": dict(workload="cfg1: 2D double integrator, MLP noise-net, CFG-DDPM (reference CPU-sized case)",
+                 system="double_int2d", net="mlp", d=2, H=16, C=4, N=50, B=64, split=False, sampler="ddpm_cfg",
+                 ddim_steps=None, schedule="exponential", dtype="f32x3", mac=117504, mac_row=93184),
+    "cfg2": dict(workload="cfg2: 2D double integrator, MLP noise-net, CFG-DDPM", system="double_int2d", net="mlp",
+                 d=2, H=32, C=4, N=100, B=4096, split=False, sampler="ddpm_cfg", ddim_steps=None,
+                 schedule="exponential", dtype="f32x3", mac=119552, mac_row=95232),
+    "cfg3": dict(workload="cfg3: pendulum swing-up, 1D temporal U-Net, CFG-DDIM (100 sampling steps)",
+                 system="pendulum", net="unet", d=1, H=32, C=2, N=100, B=16384, split=False, sampler="ddim_cfg",
+                 ddim_steps=100, schedule="exponential", dtype="f32x3", mac=9122560 + 896 * (2 - 5), mac_row=None),
+    "cfg4": dict(workload="cfg4: cart-pole (nonlinear NMPC dynamics), 1D temporal U-Net, CFG-DDPM, H=64",
+                 system="cartpole_nl5", net="unet", d=1, H=64, C=5, N=100, B=65536, split=True, sampler="ddpm_cfg",
+                 ddim_steps=None, schedule="exponential", dtype="f32x3", mac=18209152, mac_row=None),
+    "cfg5": dict(workload="cfg5: 12-DoF quadrotor, 1D temporal U-Net with fp16 GEMM operands, CFG-DDPM 250 steps",
+                 system="quadrotor12", net="unet", d=4, H=64, C=12, N=250, B=131072, split=True, sampler="ddpm_cfg",
+                 ddim_steps=None, schedule="cosine", dtype="f16", mac=18258432, mac_row=None),
+}
 PEAK_FP32 = 157.3e12      # MI355X dense fp32 MFMA / vector peak, FLOP/s (MI355X_MICROARCH.md)
-PEAK_BF16 = 2516.6e12     # MI355X dense bf16 MFMA peak: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz
-PMC_FILES = {"f32": os.path.join(ROOT, "profiles", "r1_pmc_mlp_sampler.json"),
-             "f32x3": os.path.join(ROOT, "profiles", "r1_pmc_mlp_x3.json")}
+PEAK_BF16 = 2516.6e12     # MI355X dense bf16 / fp16 MFMA peak: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz
+PMC_FILES = {("cfg2", "f32"): os.path.join(ROOT, "profiles", "r1_pmc_mlp_sampler.json"),
+             ("cfg2", "f32x3"): os.path.join(ROOT, "profiles", "r1_pmc_mlp_x3.json")}
 
 
 def _rank_env():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
 
 
-def cpu_baseline(budget_s=12.0, b_cpu=256):
+def _net(cfg):
+    from oracle import nets  # random-init weights of the net's architecture (seed 0), test infra only
+    torch.manual_seed(0)
+    if cfg["net"] == "mlp":
+        return nets.ConditionedMLPNet(state_dim=cfg["d"], horizon=cfg["H"], context_dim=cfg["C"]).eval()
+    return nets.ConditionedTemporalUnet(state_dim=cfg["d"], context_dim=cfg["C"]).eval()
+
+
+def cpu_baseline(cfg, budget_s=12.0):
     """The oracle (torch-CPU restatement of the reference path, 'port') on this host's cores:
-    normalise -> CFG-DDPM (2 forwards/step) -> unnormalise -> fp64 C rollout/cost -> argmin."""
-    from oracle import nets, normalizer, sampler, schedule
+    normalise -> CFG sampler (2 forwards/step) -> unnormalise -> fp64 C rollout/cost -> argmin."""
+    from oracle import normalizer, sampler, schedule
     from oracle import systems as osys
     threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
     torch.set_num_threads(threads)
-    torch.manual_seed(0)
-    net = nets.ConditionedMLPNet(state_dim=CFG["d"], horizon=CFG["H"], context_dim=CFG["C"]).eval()
-    bufs = schedule.buffers(CFG["schedule"], CFG["N"])
+    b_cpu = min(cfg["B"], 256 if cfg["net"] == "mlp" else 16)
+    net = _net(cfg)
+    bufs = schedule.buffers(cfg["schedule"], cfg["N"])
     rng = np.random.default_rng(1)
-    one = torch.ones(CFG["C"], dtype=torch.float32)
+    one = torch.ones(cfg["C"], dtype=torch.float32)
     done, t0 = 0, time.perf_counter()
     while True:
-        x0 = rng.uniform(-1, 1, CFG["C"])
-        ctx = normalizer.normalize(torch.from_numpy(x0)[None], -one, one).float()
-        x = sampler.ddpm_cfg(net, bufs, ctx.expand(b_cpu, CFG["C"]), CFG["w"], b_cpu, CFG["H"])
-        u = normalizer.unnormalize(x, -torch.ones(CFG["d"]), torch.ones(CFG["d"]))
-        cost = osys.rollout_cost(CFG["system"], x0, u.double().numpy())
+        x0 = rng.uniform(-1, 1, cfg["C"])
+        ctx = normalizer.normalize(torch.from_numpy(x0)[None], -one, one).float().expand(b_cpu, cfg["C"])
+        if cfg["sampler"] == "ddim_cfg":
+            x = sampler.ddim_cfg(net, bufs, ctx, 0.01, b_cpu, cfg["H"], sampling_steps=cfg["ddim_steps"])
+        else:
+            x = sampler.ddpm_cfg(net, bufs, ctx, 0.01, b_cpu, cfg["H"])
+        u = normalizer.unnormalize(x, -torch.ones(cfg["d"]), torch.ones(cfg["d"]))
+        cost = osys.rollout_cost(cfg["system"], x0, u.double().numpy())
         osys.argmin(cost)
         done += b_cpu
         el = time.perf_counter() - t0
         if el >= budget_s:
             break
     return {"value": done / el, "unit": "candidate trajectories/s", "cores": threads, "kind": "port",
-            "sample": f"{done // b_cpu} mpc_steps x {b_cpu} candidates (N=100, H=32) in {el:.1f} s; "
-                      "linear in B"}
+            "sample": f"{done // b_cpu} mpc_steps x {b_cpu} candidates (N={cfg['N']}, H={cfg['H']}) in {el:.1f} s; "
+                      "per-candidate cost is linear in B"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None, help="timed control steps (default 20; U-Net configs 3)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed control steps (default 3; U-Net configs 1)")
+    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--dtype", default="f32x3", choices=["f32", "f32x3"],
-                    help="MLP GEMM numerics: exact fp32 MFMA, or fp32-accurate split-bf16 MFMA")
+    ap.add_argument("--dtype", default=None, choices=["f32", "f32x3", "f16"],
+                    help="GEMM numerics: exact fp32 MFMA, fp32-accurate split-bf16 MFMA, fp16 operands (U-Net)")
     args = ap.parse_args()
-
+    cfg = dict(WORKLOADS[args.workload])
+    dtype = args.dtype or cfg["dtype"]
+    unet = cfg["net"] == "unet"
+    steps = args.steps if args.steps is not None else (3 if unet else 20)
+    warmup = args.warmup if args.warmup is not None else (1 if unet else 3)
     rank, world, local = _rank_env()
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -85,35 +122,41 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
+    if cfg["split"]:
+        if cfg["B"] % world:
+            raise SystemExit(f"{args.workload}: {cfg['B']} candidates do not split over {world} ranks")
+        b_local, scaling = cfg["B"] // world, "strong"
+    else:
+        b_local, scaling = cfg["B"], "weak"
 
     from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec, systems
     from mpc_via_diffusion_model_amd import distributed as D
-    from oracle import nets  # random-init weights of the net's architecture (seed 0), test infra only
 
-    torch.manual_seed(0)
-    net = nets.ConditionedMLPNet(state_dim=CFG["d"], horizon=CFG["H"], context_dim=CFG["C"])
-    spec = NetSpec("mlp", state_dim=CFG["d"], horizon=CFG["H"], context_dim=CFG["C"], dtype=args.dtype)
-    plan = DiffusionMPC(spec, net.state_dict(), variance_schedule=CFG["schedule"], n_diffusion_steps=CFG["N"])
+    net = _net(cfg)
+    spec = NetSpec(cfg["net"], state_dim=cfg["d"], horizon=cfg["H"], context_dim=cfg["C"], dtype=dtype)
+    plan = DiffusionMPC(spec, net.state_dict(), variance_schedule=cfg["schedule"], n_diffusion_steps=cfg["N"])
     del net
-    system = systems.get(CFG["system"])
+    system = systems.get(cfg["system"])
+    assert system.n_x == cfg["C"] and system.n_u == cfg["d"]
     rng = np.random.default_rng(1)
-    x0s = rng.uniform(-1, 1, (args.warmup + args.steps, system.n_x))
-
+    x0s = rng.uniform(-1, 1, (warmup + steps, system.n_x))
+    n_evals = plan.n_denoise_steps(cfg["sampler"], 0, cfg["ddim_steps"])  # CFG steps (2 forwards each)
     # the per-step exchange runs inside libmpcd.so (RCCL communicator of the planner's context)
     comm = D.NativeComm(plan) if world > 1 else None
 
     def step(i):  # one mpcd_mpc_step call: sample, clip flag, rollout/cost, select, one D2H copy
-        return plan.mpc_step(x0s[i], system, CFG["B"], w=CFG["w"], seed=2 + i, comm=comm)
+        return plan.mpc_step(x0s[i], system, b_local, w=0.01, sample_fn=cfg["sampler"], ddim_steps=cfg["ddim_steps"],
+                             seed=2 + i, comm=comm)
 
-    for i in range(args.warmup):
+    for i in range(warmup):
         step(i)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     kernel_ms = []
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        r = step(args.warmup + i)
+    for i in range(steps):
+        r = step(warmup + i)
         kernel_ms.append(plan.last_sample_ms())
     if world > 1:
         dist.barrier()
@@ -127,50 +170,66 @@ def main():
         kms = float(np.mean(kernel_ms))
 
     if rank == 0:
-        total = CFG["B"] * world * args.steps
-        flops_launch = CFG["B"] * CFG["N"] * 2 * 2 * MAC_FWD   # survey's algorithmic count (fp32 FLOPs)
+        total = b_local * world * steps
+        flops_launch = b_local * n_evals * 2 * 2 * cfg["mac"]   # survey's algorithmic count (fp32 FLOPs)
         achieved = flops_launch / (kms * 1e-3)
-        if args.dtype == "f32x3":
-            # executed matrix-core work: six bf16 partial products per fp32 MAC of the per-row Linears
-            mfma_flops = CFG["B"] * 2 * CFG["N"] * MAC_ROW * 2 * 6
+        if not unet:
+            kname = {"f32": "mlp_sample_kernel<%d,DDPM_CFG,ctx>", "f32x3": "mlp_x3_kernel<%d,DDPM_CFG,ctx>"}[dtype] % (
+                cfg["H"] * cfg["d"])
+            timed = f"{kname}: the whole denoising loop in one persistent launch (HIP events on the call's stream)"
+        else:
+            kname = "conv_mx_kernel<kind,planes,NN,NC> family" if dtype != "f32" else "conv_kernel family"
+            timed = ("one mpcd_sample call: every U-Net conv launch of the loop + the per-step update kernels "
+                     "(HIP events on the call's stream); the convs are >99% of it (profiles/)")
+        if dtype == "f32x3":
+            mac_exec = cfg["mac_row"] if cfg["mac_row"] else cfg["mac"]
+            mfma_flops = b_local * 2 * n_evals * mac_exec * 2 * 6   # six bf16 partial products per fp32 MAC
             roof = {"bound": "mfma", "achieved": mfma_flops / (kms * 1e-3) / 1e12, "peak": PEAK_BF16 / 1e12,
                     "unit": "TFLOP/s", "frac": mfma_flops / (kms * 1e-3) / PEAK_BF16,
-                    "peak_note": "bf16 dense MFMA peak; the kernel computes fp32-accurate GEMMs as 3-way bf16 splits",
+                    "peak_note": "bf16 dense MFMA peak; the kernels compute fp32-accurate GEMMs as 3-way bf16 splits "
+                                 "(6 partial products per fp32 MAC)",
                     "fp32_equiv": {"achieved": achieved / 1e12, "peak": PEAK_FP32 / 1e12,
                                    "frac": achieved / PEAK_FP32, "flop_per_launch": flops_launch},
-                    "kernel": "mlp_x3_kernel<64,DDPM_CFG,ctx>", "flop_per_launch": mfma_flops}
+                    "kernel": kname, "flop_per_launch": mfma_flops}
+        elif dtype == "f16":
+            roof = {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
+                    "frac": achieved / PEAK_BF16, "peak_note": "fp16 dense MFMA peak", "kernel": kname,
+                    "flop_per_launch": flops_launch}
         else:
             roof = {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP32 / 1e12, "unit": "TFLOP/s",
-                    "frac": achieved / PEAK_FP32, "kernel": "mlp_sample_kernel<64,DDPM_CFG,ctx>",
-                    "flop_per_launch": flops_launch}
+                    "frac": achieved / PEAK_FP32, "kernel": kname, "flop_per_launch": flops_launch}
         traffic = None
-        if os.path.exists(PMC_FILES[args.dtype]):
-            with open(PMC_FILES[args.dtype]) as f:
+        pmc = PMC_FILES.get((args.workload, dtype))
+        if pmc and os.path.exists(pmc):
+            with open(pmc) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
+        gemm = {"f32": "exact fp32 MFMA (v_mfma_f32_16x16x4_f32)",
+                "f32x3": "fp32-accurate split-bf16 MFMA (3 bf16 terms per operand, 6 partial products, fp32 accumulate)",
+                "f16": "fp16 operands, fp32 accumulate (v_mfma_f32_16x16x32_f16)"}[dtype]
         out = {
-            "metric": "candidate trajectories/sec (100 denoise steps, H=32)",
+            "metric": "candidate trajectories/sec (100 denoise steps, H=32)" if args.workload == "cfg2" else
+                      f"candidate trajectories/sec ({n_evals} denoise steps, H={cfg['H']})",
             "value": total / elapsed,
             "unit": "candidate trajectories/s",
             "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": 1e3 * elapsed / args.steps,
+            "steps": steps,
+            "warmup": warmup,
+            "ms_per_step": 1e3 * elapsed / steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (random-init weights seed 0, x0 ~ U[-1,1]^4, Philox noise)",
-            "config": {"workload": CFG["workload"], "candidates_per_gpu": CFG["B"], "horizon": CFG["H"],
-                       "action_dim": CFG["d"], "context_dim": CFG["C"], "denoise_steps": CFG["N"],
-                       "sampler": "CFG-DDPM w=0.01", "schedule": CFG["schedule"], "parallelism": f"dp{world}",
-                       "gemm": {"f32": "exact fp32 MFMA (v_mfma_f32_16x16x4_f32)",
-                                "f32x3": "fp32-accurate split-bf16 MFMA (3 bf16 terms per operand, 6 partial "
-                                         "products, fp32 accumulate)"}[args.dtype]},
-            "roofline": dict(roof, traffic=traffic, kernel_ms=kms),
+            "dtype": "f16" if dtype == "f16" else "f32",
+            "data": f"synthetic (random-init weights seed 0, x0 ~ U[-1,1]^{cfg['C']}, Philox noise)",
+            "config": {"workload": cfg["workload"], "candidates_per_gpu": b_local, "candidates_total": b_local * world,
+                       "horizon": cfg["H"], "action_dim": cfg["d"], "context_dim": cfg["C"], "denoise_steps": n_evals,
+                       "sampler": f"{'CFG-DDIM' if cfg['sampler'] == 'ddim_cfg' else 'CFG-DDPM'} w=0.01",
+                       "schedule": cfg["schedule"], "noise_net": cfg["net"], "parallelism": f"dp{world}",
+                       "gemm": gemm},
+            "roofline": dict(roof, traffic=traffic, kernel_ms=kms, timed=timed),
             "best_cost_last_step": r.best_cost,
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_budget)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
