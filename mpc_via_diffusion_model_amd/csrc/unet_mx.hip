@@ -92,19 +92,49 @@ constexpr int NPROD(int P) { return P == 1 ? 1 : 6; }
 template <int P> constexpr int PA(int i) { return P == 1 ? 0 : i == 0 ? 2 : i == 1 ? 1 : i == 2 ? 0 : i == 3 ? 1 : 0; }
 template <int P> constexpr int PB(int i) { return P == 1 ? 0 : i == 0 ? 0 : i == 1 ? 1 : i == 2 ? 2 : i == 3 ? 0 : i == 4 ? 1 : 0; }
 
-// (tap, first channel) of lane quarter q in k-chunk kc; cinp is 8, 16 or a multiple of 32
-MPCD_DEV void tap_of(int kc, int q, int cinp, int &tap, int &ci0)
+// n / d and n % d for small non-negative n (< 2^20) via a float reciprocal + one correction step:
+// a handful of VALU ops instead of the ~20-op integer division sequence.
+MPCD_DEV int qdiv(int n, int d, float inv_d, int &rem)
 {
-    if (cinp >= 32) {
-        const int cpt = cinp >> 5;  // chunks per tap
-        tap = kc / cpt;
-        ci0 = (kc - tap * cpt) * 32 + 8 * q;
-    } else {
-        const int tpc = 32 / cinp;  // taps per chunk
-        tap = kc * tpc + (8 * q) / cinp;
-        ci0 = (8 * q) % cinp;
-    }
+    int q = (int)((float)n * inv_d);
+    int r = n - q * d;
+    if (r < 0) { --q; r += d; }
+    if (r >= d) { ++q; r -= d; }
+    rem = r;
+    return q;
 }
+
+// Walks the K chunks of one lane quarter q: chunk kc covers, for this lane, 8 consecutive channels
+// of one tap (cinp >= 32: 32/cinp... chunks per tap; cinp 8 / 16: 4 / 2 taps per chunk). koff() is
+// the byte offset of those 8 channels in the staged window relative to the column's tap-0 position.
+struct KWalk {
+    int tap, ci0, cpt, tpc, cinp;
+    MPCD_DEV void init(int q, int cinp_)
+    {
+        cinp = cinp_;
+        if (cinp >= 32) {
+            cpt = cinp >> 5;
+            tpc = 0;
+            tap = 0;
+            ci0 = 8 * q;
+        } else {
+            cpt = 0;
+            tpc = 32 / cinp;
+            tap = (8 * q) / cinp;
+            ci0 = (8 * q) % cinp;
+        }
+    }
+    MPCD_DEV void next()
+    {
+        if (cpt) {
+            ci0 += 32;
+            if (ci0 >= cinp) { ci0 -= cinp; ++tap; }
+        } else {
+            tap += tpc;
+        }
+    }
+    template <int KIND> MPCD_DEV int koff(int cs) const { return (KIND == UCONV_UP4 ? -tap : tap) * cs + 2 * ci0; }
+};
 
 template <int KIND, int P, int NN, int NC>
 __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
@@ -136,8 +166,11 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
 
     // ---- stage the input window, split into P planes (zero outside [0, lin), padded channels, rows >= nrow)
     const int g8n = a.cinp >> 3, cin = a.ca + a.cb;
+    const float inv_g8n = 1.0f / (float)g8n, inv_win = 1.0f / (float)win;
     for (int i = tid; i < a.rb * win * g8n; i += MT) {
-        const int g8 = i % g8n, pw = (i / g8n) % win, r = i / (g8n * win);
+        int g8, pw;
+        const int rp = qdiv(i, g8n, inv_g8n, g8);
+        const int r = qdiv(rp, win, inv_win, pw);
         const int p = pw - a.halo_l, ci = 8 * g8;
         f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
         if (r < nrow && p >= 0 && p < a.lin) {
@@ -229,20 +262,14 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
                 }
             }
         };
-        u32x4 A[NN][P];
-        load_a(A, 0);
-        for (int kc = 0; kc < KC; ++kc) {
-            int tap, ci0;
-            tap_of(kc, q, a.cinp, tap, ci0);
-            const int koff = (KIND == UCONV_UP4 ? -tap : tap) * a.cs + 2 * ci0;
-            u32x4 B[NC][P];
+        auto load_b = [&](u32x4 (&B)[NC][P], int koff) {
 #pragma unroll
             for (int cc = 0; cc < NC; ++cc)
 #pragma unroll
                 for (int pl = 0; pl < P; ++pl)
                     B[cc][pl] = *reinterpret_cast<const u32x4 *>(sm + pl * planeB + bb[cc] + koff);
-            u32x4 An[NN][P];
-            if (kc + 1 < KC) load_a(An, kc + 1);
+        };
+        auto mmas = [&](const u32x4 (&A)[NN][P], const u32x4 (&B)[NC][P]) {
 #pragma unroll
             for (int i = 0; i < NPROD(P); ++i)
 #pragma unroll
@@ -250,11 +277,48 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
 #pragma unroll
                     for (int cc = 0; cc < NC; ++cc)
                         acc[j][cc] = mma<P>(A[j][PA<P>(i)], B[cc][PB<P>(i)], acc[j][cc]);
-            if (kc + 1 < KC) {
+        };
+        // A (weights, L2) runs DA chunks ahead in a register ring; B (LDS) one chunk ahead. The
+        // prefetches are unconditional (clamped to the last chunk) so the waits before each chunk's
+        // MFMAs leave the younger loads in flight.
+        constexpr int DA = P == 1 ? (NN * NC >= 32 ? 2 : 4) : 2;
+        u32x4 A[DA][NN][P];
 #pragma unroll
-                for (int j = 0; j < NN; ++j)
+        for (int s = 0; s < DA; ++s) load_a(A[s], min(s, KC - 1));
+        KWalk kw;
+        kw.init(q, a.cinp);
+        u32x4 Bc[NC][P], Bn[NC][P];
+        load_b(Bc, kw.koff<KIND>(a.cs));
+        int kc = 0;
+        for (; kc + DA <= KC; kc += DA) {
 #pragma unroll
-                    for (int pl = 0; pl < P; ++pl) A[j][pl] = An[j][pl];
+            for (int s = 0; s < DA; ++s) {
+                KWalk kn = kw;
+                kn.next();
+                const bool more = kc + s + 1 < KC;
+                load_b(Bn, more ? kn.koff<KIND>(a.cs) : kw.koff<KIND>(a.cs));
+                mmas(A[s], Bc);
+                load_a(A[s], min(kc + s + DA, KC - 1));
+#pragma unroll
+                for (int cc = 0; cc < NC; ++cc)
+#pragma unroll
+                    for (int pl = 0; pl < P; ++pl) Bc[cc][pl] = Bn[cc][pl];
+                kw = kn;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < DA - 1; ++s) {  // tail: KC % DA chunks, A[s] holds chunk kc + s
+            if (kc + s < KC) {
+                KWalk kn = kw;
+                kn.next();
+                const bool more = kc + s + 1 < KC;
+                load_b(Bn, more ? kn.koff<KIND>(a.cs) : kw.koff<KIND>(a.cs));
+                mmas(A[s], Bc);
+#pragma unroll
+                for (int cc = 0; cc < NC; ++cc)
+#pragma unroll
+                    for (int pl = 0; pl < P; ++pl) Bc[cc][pl] = Bn[cc][pl];
+                kw = kn;
             }
         }
     };
@@ -329,8 +393,11 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
 
     // ---- epilogue + store: thread per (row, position, channel quad); per-channel operands from LDS
     const int cq = (a.cout + 3) >> 2;
+    const float inv_cq = 1.0f / (float)cq, inv_lout = 1.0f / (float)a.lout;
     for (int i = tid; i < nrow * a.lout * cq; i += MT) {
-        const int q4 = i % cq, oo = (i / cq) % a.lout, r = i / (cq * a.lout);
+        int q4, oo;
+        const int ro = qdiv(i, cq, inv_cq, q4);
+        const int r = qdiv(ro, a.lout, inv_lout, oo);
         const int co = 4 * q4;
         const f32x4 raw = *reinterpret_cast<const f32x4 *>(s_out + (size_t)colof(r, oo) * sout + co);
         const int64_t grow = r0 + r;
