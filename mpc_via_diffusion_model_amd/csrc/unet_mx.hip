@@ -136,16 +136,21 @@ struct KWalk {
     template <int KIND> MPCD_DEV int koff(int cs) const { return (KIND == UCONV_UP4 ? -tap : tap) * cs + 2 * ci0; }
 };
 
-template <int KIND, int P, int NN, int NC>
+// PERS = false: one row block per workgroup (grid = blocks). PERS = true: a resident grid walks the
+// row blocks; while block b runs its GEMM / statistics / epilogue, the 16-byte loads of block b+grid's
+// input window are already in flight (registers), and are converted into the (non-aliased) staging
+// area once b's GEMM has finished reading it.
+constexpr int SUP = 6;  // staging items per thread a persistent workgroup keeps in flight (host-checked)
+
+template <int KIND, int P, int NN, int NC, bool PERS>
 __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
 {
     extern __shared__ __attribute__((aligned(16))) char sm[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int64_t r0 = (int64_t)blockIdx.x * a.rb;
-    const int nrow = (int)min((int64_t)a.rb, a.rows - r0);
     const int win = a.lin + a.halo_l + a.halo_r;
     const int rowB = win * a.cs, planeB = a.rb * rowB;
+    const int64_t nblocks = (a.rows + a.rb - 1) / a.rb;
     float *s_stat = reinterpret_cast<float *>(sm + a.stat_off);  // [rb][groups][mean, rstd]
     // [4][coutp]: gn_w, gn_b, cond of the context rows (tproj + shared cproj), cond of the masked rows (tproj)
     float *s_chan = s_stat + 2 * a.rb * 32 + 4;
@@ -164,45 +169,99 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
         }
     }
 
-    // ---- stage the input window, split into P planes (zero outside [0, lin), padded channels, rows >= nrow)
+    // ---- staging of a row block's input window, split into P planes (zero outside [0, lin), padded
+    // channels, rows past the batch)
     const int g8n = a.cinp >> 3, cin = a.ca + a.cb;
     const float inv_g8n = 1.0f / (float)g8n, inv_win = 1.0f / (float)win;
-    for (int i = tid; i < a.rb * win * g8n; i += MT) {
+    const int n_items = a.rb * win * g8n;
+    // input row of staged row r: rows >= x_rows re-read the first x_rows (CFG's branches share x)
+    auto xrow = [&](int64_t r0, int r) {
+        int64_t xr = r0 + r;
+        while (xr >= a.x_rows) xr -= a.x_rows;
+        return xr;
+    };
+    // one 16-byte item (8 channels of one position of one row): source pointer (or null = zeros), LDS dest
+    auto item = [&](int64_t r0, int nrow, int i, const float *&src, int &dst) {
         int g8, pw;
         const int rp = qdiv(i, g8n, inv_g8n, g8);
         const int r = qdiv(rp, win, inv_win, pw);
         const int p = pw - a.halo_l, ci = 8 * g8;
-        f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
-        if (r < nrow && p >= 0 && p < a.lin) {
-            const int64_t xr = (r0 + r) % a.x_rows;
-            if ((a.ca & 7) == 0 && ci + 8 <= a.ca) {
-                const float *s = a.xa + ((size_t)xr * a.lin + p) * a.ca + ci;
-                lo = ldg4(s);
-                hi = ldg4(s + 4);
-            } else if ((a.ca & 7) == 0 && (a.cb & 7) == 0 && ci >= a.ca && ci + 8 <= cin) {
-                const float *s = a.xb + ((size_t)xr * a.lin + p) * a.cb + (ci - a.ca);
-                lo = ldg4(s);
-                hi = ldg4(s + 4);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const int c = ci + e;
-                    float v = 0.f;
-                    if (c < a.ca) v = a.xa[((size_t)xr * a.lin + p) * a.ca + c];
-                    else if (c < cin) v = a.xb[((size_t)xr * a.lin + p) * a.cb + (c - a.ca)];
-                    if (e < 4) lo[e] = v; else hi[e - 4] = v;
-                }
-            }
+        dst = r * rowB + pw * a.cs + g8 * 16;
+        src = nullptr;
+        if (r < nrow && p >= 0 && p < a.lin && ci < cin) {
+            const int64_t xr = xrow(r0, r);
+            src = ci < a.ca ? a.xa + ((size_t)xr * a.lin + p) * a.ca + ci
+                            : a.xb + ((size_t)xr * a.lin + p) * a.cb + (ci - a.ca);
         }
+    };
+    auto put = [&](int dst, const f32x4 &lo, const f32x4 &hi) {
         u32x4 o[P];
         split8<P>(lo, hi, o);
 #pragma unroll
-        for (int pl = 0; pl < P; ++pl)
-            *reinterpret_cast<u32x4 *>(sm + pl * planeB + r * rowB + pw * a.cs + g8 * 16) = o[pl];
-    }
-    __syncthreads();
+        for (int pl = 0; pl < P; ++pl) *reinterpret_cast<u32x4 *>(sm + pl * planeB + dst) = o[pl];
+    };
+    auto stage_direct = [&](int64_t r0, int nrow) {
+        if ((a.ca & 7) == 0 && (a.cb & 7) == 0) {
+            constexpr int SU = 4;  // items per thread in flight before any conversion or LDS store
+            for (int i0 = tid; i0 < n_items; i0 += SU * MT) {
+                f32x4 lo[SU], hi[SU];
+                int dst[SU];
+#pragma unroll
+                for (int u = 0; u < SU; ++u) {
+                    const float *src;
+                    item(r0, nrow, min(i0 + u * MT, n_items - 1), src, dst[u]);
+                    lo[u] = ldg4(src ? src : a.xa);
+                    hi[u] = ldg4(src ? src + 4 : a.xa);
+                    if (!src) lo[u] = hi[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+#pragma unroll
+                for (int u = 0; u < SU; ++u)
+                    if (i0 + u * MT < n_items) put(dst[u], lo[u], hi[u]);
+            }
+        } else {  // channel counts not multiples of 8 (the first layer: d channels): scalar loads
+            for (int i = tid; i < n_items; i += MT) {
+                int g8, pw;
+                const int rp = qdiv(i, g8n, inv_g8n, g8);
+                const int r = qdiv(rp, win, inv_win, pw);
+                const int p = pw - a.halo_l, ci = 8 * g8;
+                f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
+                if (r < nrow && p >= 0 && p < a.lin) {
+                    const int64_t xr = xrow(r0, r);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const int c = ci + e;
+                        float v = 0.f;
+                        if (c < a.ca) v = a.xa[((size_t)xr * a.lin + p) * a.ca + c];
+                        else if (c < cin) v = a.xb[((size_t)xr * a.lin + p) * a.cb + (c - a.ca)];
+                        if (e < 4) lo[e] = v; else hi[e - 4] = v;
+                    }
+                }
+                put(r * rowB + pw * a.cs + g8 * 16, lo, hi);
+            }
+        }
+    };
+    // persistent prefetch: issue (loads into registers) / commit (convert + LDS stores)
+    f32x4 pre_lo[PERS ? SUP : 1], pre_hi[PERS ? SUP : 1];
+    int pre_dst[PERS ? SUP : 1];
+    auto stage_issue = [&](int64_t r0, int nrow) {
+#pragma unroll
+        for (int u = 0; u < (PERS ? SUP : 1); ++u) {
+            const int i = tid + u * MT;
+            const float *src;
+            item(r0, nrow, min(i, n_items - 1), src, pre_dst[u]);
+            if (i >= n_items) pre_dst[u] = -1;
+            pre_lo[u] = ldg4(src ? src : a.xa);
+            pre_hi[u] = ldg4(src ? src + 4 : a.xa);
+            if (!src) pre_lo[u] = pre_hi[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    auto stage_commit = [&]() {
+#pragma unroll
+        for (int u = 0; u < (PERS ? SUP : 1); ++u)
+            if (pre_dst[u] >= 0) put(pre_dst[u], pre_lo[u], pre_hi[u]);
+    };
 
-    // ---- implicit GEMM
+    // ---- implicit GEMM geometry
     const int NT = a.coutp >> 4, KC = a.kc;
     const int npar = KIND == UCONV_UP4 ? 2 : 1;
     const int nval = KIND == UCONV_UP4 ? a.rb * a.lin : a.rb * a.lout;  // real columns per parity block
@@ -337,26 +396,14 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
             }
         }
     };
-    if (a.alias) {  // one job per wave (host-checked): finish every read of the staged input first
-        if (wave < jobs) compute(wave);
-        __syncthreads();
-        if (wave < jobs) store(wave);
-    } else {
-        for (int job = wave; job < jobs; job += MT / 64) {
-            compute(job);
-            store(job);
-        }
-    }
-    __syncthreads();
-
     auto colof = [&](int r, int oo) -> int {
         if (KIND == UCONV_UP4) return (oo & 1) * cpar16 + r * a.lin + (oo >> 1);
         return r * a.lout + oo;
     };
+    const int epi = a.epi, gsh = a.cpg_shift;  // cpg = cout / groups = 1 << gsh (host-checked, >= 4)
 
     // ---- GroupNorm statistics per (row, group): fp64, shifted by the group's first value, tpp lanes each
-    const int epi = a.epi, gsh = a.cpg_shift;  // cpg = cout / groups = 1 << gsh (host-checked, >= 4)
-    if (epi != UEPI_BIAS) {
+    auto stats = [&](int nrow) {
         const int pairs = nrow * a.groups, nq = a.lout << (gsh - 2);  // channel quads per (row, group)
         int tpp = 1;
         while (tpp < 64 && tpp * 2 * pairs <= MT) tpp *= 2;
@@ -388,46 +435,110 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
             s_stat[2 * pi] = (float)((double)ref + ms);
             s_stat[2 * pi + 1] = (float)(1.0 / sqrt(var + 1e-5));
         }
-        __syncthreads();
-    }
+    };
 
     // ---- epilogue + store: thread per (row, position, channel quad); per-channel operands from LDS
     const int cq = (a.cout + 3) >> 2;
     const float inv_cq = 1.0f / (float)cq, inv_lout = 1.0f / (float)a.lout;
-    for (int i = tid; i < nrow * a.lout * cq; i += MT) {
-        int q4, oo;
-        const int ro = qdiv(i, cq, inv_cq, q4);
-        const int r = qdiv(ro, a.lout, inv_lout, oo);
-        const int co = 4 * q4;
-        const f32x4 raw = *reinterpret_cast<const f32x4 *>(s_out + (size_t)colof(r, oo) * sout + co);
-        const int64_t grow = r0 + r;
-        f32x4 v = raw;
-        if (epi != UEPI_BIAS) {
-            const int g = co >> gsh;
-            const float mean = s_stat[2 * (r * a.groups + g)], rstd = s_stat[2 * (r * a.groups + g) + 1];
-            const f32x4 gw = *reinterpret_cast<const f32x4 *>(s_chan + co);
-            const f32x4 gb = *reinterpret_cast<const f32x4 *>(s_chan + a.coutp + co);
+    auto epilogue = [&](int64_t r0, int nrow) {
+        const int n_out = nrow * a.lout * cq;
+        constexpr int EU = 4;  // items per thread with their residual loads in flight together
+        for (int i0 = tid; i0 < n_out; i0 += EU * MT) {
+            f32x4 rv[EU];
+            int rr[EU], ro_[EU], cc_[EU];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float scale = rstd * gw[e];
-                const float shift = -scale * mean + gb[e];
-                v[e] = mish(raw[e] * scale + shift);
+            for (int u = 0; u < EU; ++u) {
+                const int i = min(i0 + u * MT, n_out - 1);  // clamped: a duplicate item is recomputed, not stored
+                int q4, oo;
+                const int ro = qdiv(i, cq, inv_cq, q4);
+                rr[u] = qdiv(ro, a.lout, inv_lout, oo);
+                ro_[u] = oo;
+                cc_[u] = 4 * q4;
+                if (epi == UEPI_GN_MISH_RES)
+                    rv[u] = ldg4(a.res + ((size_t)(r0 + rr[u]) * a.lout + oo) * a.cout + cc_[u]);
             }
-            if (epi == UEPI_GN_MISH_COND) {  // row < b_cand: context branch; else the masked (CFG) branch
-                const int64_t br = grow / a.b_cand, cand = grow - br * a.b_cand;
-                f32x4 cv = *reinterpret_cast<const f32x4 *>(s_chan + (br == 0 ? 2 : 3) * a.coutp + co);
-                if (a.cp && a.cp_stride && br == 0)
-                    cv = cv + *reinterpret_cast<const f32x4 *>(a.cp + (size_t)cand * a.cp_stride + co);
-                v = v + cv;
+#pragma unroll
+            for (int u = 0; u < EU; ++u) {
+                if (i0 + u * MT >= n_out) break;
+                const int r = rr[u], oo = ro_[u], co = cc_[u];
+                const f32x4 raw = *reinterpret_cast<const f32x4 *>(s_out + (size_t)colof(r, oo) * sout + co);
+                const int64_t grow = r0 + r;
+                f32x4 v = raw;
+                if (epi != UEPI_BIAS) {
+                    const int g = co >> gsh;
+                    const float mean = s_stat[2 * (r * a.groups + g)], rstd = s_stat[2 * (r * a.groups + g) + 1];
+                    const f32x4 gw = *reinterpret_cast<const f32x4 *>(s_chan + co);
+                    const f32x4 gb = *reinterpret_cast<const f32x4 *>(s_chan + a.coutp + co);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float scale = rstd * gw[e];
+                        const float shift = -scale * mean + gb[e];
+                        v[e] = mish(raw[e] * scale + shift);
+                    }
+                    if (epi == UEPI_GN_MISH_COND) {  // row < b_cand: context branch; else the masked (CFG) branch
+                        int64_t cand = grow, br = 0;  // branch = row / b_cand (0: context, 1: masked)
+                        while (cand >= a.b_cand) { cand -= a.b_cand; ++br; }
+                        f32x4 cv = *reinterpret_cast<const f32x4 *>(s_chan + (br == 0 ? 2 : 3) * a.coutp + co);
+                        if (a.cp && a.cp_stride && br == 0)
+                            cv = cv + *reinterpret_cast<const f32x4 *>(a.cp + (size_t)cand * a.cp_stride + co);
+                        v = v + cv;
+                    }
+                    if (epi == UEPI_GN_MISH_RES) v = v + rv[u];
+                }
+                float *dst = a.out + ((size_t)grow * a.lout + oo) * a.cout + co;
+                if ((a.cout & 3) == 0) {
+                    *reinterpret_cast<f32x4 *>(dst) = v;
+                } else {
+                    for (int e = 0; e < 4 && co + e < a.cout; ++e) dst[e] = v[e];
+                }
             }
-            if (epi == UEPI_GN_MISH_RES)
-                v = v + ldg4(a.res + ((size_t)grow * a.lout + oo) * a.cout + co);
         }
-        float *dst = a.out + ((size_t)grow * a.lout + oo) * a.cout + co;
-        if ((a.cout & 3) == 0) {
-            *reinterpret_cast<f32x4 *>(dst) = v;
+    };
+
+    if constexpr (!PERS) {
+        const int64_t r0 = (int64_t)blockIdx.x * a.rb;
+        const int nrow = (int)min((int64_t)a.rb, a.rows - r0);
+        stage_direct(r0, nrow);
+        __syncthreads();
+        if (a.alias) {  // one job per wave (host-checked): finish every read of the staged input first
+            if (wave < jobs) compute(wave);
+            __syncthreads();
+            if (wave < jobs) store(wave);
         } else {
-            for (int e = 0; e < 4 && co + e < a.cout; ++e) dst[e] = v[e];
+            for (int job = wave; job < jobs; job += MT / 64) {
+                compute(job);
+                store(job);
+            }
+        }
+        __syncthreads();
+        if (epi != UEPI_BIAS) {
+            stats(nrow);
+            __syncthreads();
+        }
+        epilogue(r0, nrow);
+    } else {  // host: no alias, 16-byte staging, items per thread <= SUP
+        int64_t blk = blockIdx.x;
+        {
+            const int64_t r0 = blk * a.rb;
+            stage_issue(r0, (int)min((int64_t)a.rb, a.rows - r0));
+            stage_commit();
+        }
+        __syncthreads();
+        for (; blk < nblocks; blk += gridDim.x) {
+            const int64_t r0 = blk * a.rb;
+            const int nrow = (int)min((int64_t)a.rb, a.rows - r0);
+            const int64_t nxt = blk + gridDim.x;
+            if (nxt < nblocks) stage_issue(nxt * a.rb, (int)min((int64_t)a.rb, a.rows - nxt * a.rb));
+            for (int job = wave; job < jobs; job += MT / 64) {
+                compute(job);
+                store(job);
+            }
+            __syncthreads();  // staged input fully read, fp32 tile complete
+            if (nxt < nblocks) stage_commit();
+            if (epi != UEPI_BIAS) stats(nrow);
+            __syncthreads();
+            epilogue(r0, nrow);
+            __syncthreads();  // tile and statistics read before the next block overwrites them
         }
     }
 }
@@ -466,26 +577,47 @@ struct Tile {
 constexpr Tile kTiles3[] = {{2, 4}, {1, 8}, {1, 4}};
 constexpr Tile kTiles1[] = {{4, 8}, {2, 8}, {2, 4}, {1, 8}, {1, 4}};
 
-template <int KIND, int P, int NN, int NC>
+int g_n_cu = 0;  // compute units of the device (persistent grids)
+
+template <int KIND, int P, int NN, int NC, bool PERS>
 hipError_t launch_one(const ConvMK &k, size_t lds, hipStream_t st)
 {
+    auto *fn = reinterpret_cast<const void *>(&conv_mx_kernel<KIND, P, NN, NC, PERS>);
     static bool set = false;
+    static int resident = 0;  // workgroups per CU at this kernel's registers and the LDS of its first use
+    static size_t resident_lds = 0;
     if (!set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&conv_mx_kernel<KIND, P, NN, NC>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         set = true;
     }
-    const int64_t blocks = (k.rows + k.rb - 1) / k.rb;
-    hipLaunchKernelGGL((conv_mx_kernel<KIND, P, NN, NC>), dim3((unsigned)blocks), dim3(MT), lds, st, k);
+    int64_t blocks = (k.rows + k.rb - 1) / k.rb;
+    if (PERS) {
+        if (resident_lds != lds) {
+            int n = 0;
+            hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, MT, lds);
+            if (e != hipSuccess) return e;
+            resident = std::max(n, 1);
+            resident_lds = lds;
+        }
+        if (!g_n_cu) {
+            int dev = 0;
+            hipError_t e = hipGetDevice(&dev);
+            if (e == hipSuccess) e = hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+            if (e != hipSuccess) return e;
+        }
+        blocks = std::min<int64_t>(blocks, (int64_t)resident * g_n_cu);
+    }
+    hipLaunchKernelGGL((conv_mx_kernel<KIND, P, NN, NC, PERS>), dim3((unsigned)blocks), dim3(MT), lds, st, k);
     return hipGetLastError();
 }
 
 template <int KIND, int P>
-hipError_t launch_kind(const ConvMK &k, Tile t, size_t lds, hipStream_t st)
+hipError_t launch_kind(const ConvMK &k, Tile t, bool pers, size_t lds, hipStream_t st)
 {
-#define T_(A, B) \
-    if (t.nn == A && t.nc == B) return launch_one<KIND, P, A, B>(k, lds, st);
+#define T_(A, B)                                                                          \
+    if (t.nn == A && t.nc == B)                                                           \
+        return pers ? launch_one<KIND, P, A, B, true>(k, lds, st) : launch_one<KIND, P, A, B, false>(k, lds, st);
     if constexpr (P == 3) {
         T_(2, 4) T_(1, 8) T_(1, 4)
     } else {
@@ -498,6 +630,7 @@ hipError_t launch_kind(const ConvMK &k, Tile t, size_t lds, hipStream_t st)
 struct MxChoice {
     int rb;
     Tile t;
+    int pers;   // persistent grid with the next block's staging loads in flight
     int alias;
     size_t lds;
     int stat_off;  // LDS byte offset of the GroupNorm statistics
@@ -532,8 +665,8 @@ hipError_t launch_choice(int kind, int planes, ConvMK &k, const MxChoice &ch, hi
     k.stat_off = ch.stat_off;
 #define K_(KD)                                                                        \
     if (kind == KD)                                                                   \
-        return planes == 1 ? launch_kind<KD, 1>(k, ch.t, ch.lds, st)                  \
-                           : launch_kind<KD, 3>(k, ch.t, ch.lds, st);
+        return planes == 1 ? launch_kind<KD, 1>(k, ch.t, ch.pers, ch.lds, st)         \
+                           : launch_kind<KD, 3>(k, ch.t, ch.pers, ch.lds, st);
     K_(UCONV_SAME5)
     K_(UCONV_DOWN3)
     K_(UCONV_UP4)
@@ -654,9 +787,17 @@ hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::
                                    (t.nn * t.nc * nprod * 16.0 + t.nn * planes * 24.0 + t.nc * planes * 8.0) +
                                (double)in_b / 64.0 + 600.0;
             const double cost = cyc / rb;
-            if (!best.rb || cost < best.model * 0.999) best = MxChoice{rb, t, alias, lds, (int)body, cost};
+            if (!best.rb || cost < best.model * 0.999) best = MxChoice{rb, t, 0, alias, lds, (int)body, cost};
         }
         if (best.rb) cands.push_back(best);
+        // persistent form of the same tile: staging and fp32 tile side by side (no alias), every
+        // thread's staging items fit the in-flight registers
+        if (best.rb && (k.ca & 7) == 0 && (k.cb & 7) == 0 && (int64_t)rb * 4 < k.rows) {
+            const int items = rb * win * (cinp / 8);
+            const size_t lds = in_b + out_b + stat_b;
+            if ((items + MT - 1) / MT <= SUP && lds <= cap)
+                cands.push_back(MxChoice{rb, best.t, 1, 0, lds, (int)(in_b + out_b), best.model * 1.0001});
+        }
     }
     if (cands.empty()) {
         if (why) *why = "UNet mx conv: no tiling fits LDS";
