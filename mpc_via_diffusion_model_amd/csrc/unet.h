@@ -50,6 +50,7 @@ struct ConvMK {
     int alias;              // 1: the fp32 output tile reuses the staged-input LDS
     int stat_off;           // LDS byte offset of the GroupNorm statistics (then the per-channel table)
     int cpg_shift;          // log2(cout / groups)
+    int skip;               // experiment only (MPCD_UNET_SKIP): bit 0 staging, 1 GEMM, 2 statistics, 3 epilogue
 };
 
 struct UnetWeights {

@@ -28,6 +28,7 @@
 #include <map>
 #include <mutex>
 #include <tuple>
+#include <type_traits>
 #include <vector>
 #include <string>
 
@@ -405,91 +406,101 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
     // ---- GroupNorm statistics per (row, group): fp64, shifted by the group's first value, tpp lanes each
     auto stats = [&](int nrow) {
         const int pairs = nrow * a.groups, nq = a.lout << (gsh - 2);  // channel quads per (row, group)
-        int tpp = 1;
-        while (tpp < 64 && tpp * 2 * pairs <= MT) tpp *= 2;
-        const int pi = tid / tpp, sub = tid - pi * tpp;
-        double s1 = 0.0, s2 = 0.0;
-        float ref = 0.f;
-        if (pi < pairs) {
+        // a fixed 4 lanes per (row, group), strided over its quads, then a fixed xor tree: the summation
+        // order depends on the layer only, never on rows per workgroup or batch (results are
+        // bit-identical however the batch is sharded)
+        constexpr int TPP = 4;
+        const int sub = tid & (TPP - 1);
+        // fp64 sums for the fp32-accurate net; fp32 (shifted) sums for the fp16-operand net (P == 1),
+        // whose GEMM operands already carry 2^-11 relative rounding
+        using sum_t = typename std::conditional<P == 1, float, double>::type;
+        for (int pi = tid / TPP; pi < pairs; pi += MT / TPP) {
             const int r = pi / a.groups, g = pi - r * a.groups;
             const float *base = s_out + (g << gsh);
-            ref = base[(size_t)colof(r, 0) * sout];
-            for (int e = sub; e < nq; e += tpp) {
+            const float ref = base[(size_t)colof(r, 0) * sout];
+            sum_t s1 = 0, s2 = 0;
+            for (int e = sub; e < nq; e += TPP) {
                 const int oo = e >> (gsh - 2), cc = (e - (oo << (gsh - 2))) * 4;
                 const f32x4 v4 = *reinterpret_cast<const f32x4 *>(base + (size_t)colof(r, oo) * sout + cc);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const double v = (double)v4[k] - (double)ref;
+                    const sum_t v = (sum_t)v4[k] - (sum_t)ref;
                     s1 += v;
                     s2 += v * v;
                 }
             }
-        }
-        for (int m = 1; m < tpp; m <<= 1) {
-            s1 += __shfl_xor(s1, m);
-            s2 += __shfl_xor(s2, m);
-        }
-        if (pi < pairs && sub == 0) {
-            const double n = (double)(nq * 4), ms = s1 / n;
-            const double var = fmax(s2 / n - ms * ms, 0.0);
-            s_stat[2 * pi] = (float)((double)ref + ms);
-            s_stat[2 * pi + 1] = (float)(1.0 / sqrt(var + 1e-5));
+#pragma unroll
+            for (int m = 1; m < TPP; m <<= 1) {  // the 4 lanes of a pair are consecutive and active together
+                s1 += __shfl_xor(s1, m);
+                s2 += __shfl_xor(s2, m);
+            }
+            if (sub == 0) {
+                const double n = (double)(nq * 4), ms = (double)s1 / n;
+                const double var = fmax((double)s2 / n - ms * ms, 0.0);
+                s_stat[2 * pi] = (float)((double)ref + ms);
+                s_stat[2 * pi + 1] = (float)(1.0 / sqrt(var + 1e-5));
+            }
         }
     };
 
-    // ---- epilogue + store: thread per (row, position, channel quad); per-channel operands from LDS
+    // ---- epilogue + store: every thread keeps one channel quad (its GroupNorm affine and cond
+    // operands in registers) and walks (row, position) items; one 16-byte load / store per item
     const int cq = (a.cout + 3) >> 2;
-    const float inv_cq = 1.0f / (float)cq, inv_lout = 1.0f / (float)a.lout;
+    const int q4t = tid % cq, tps = MT / cq;  // cq divides MT (cout <= 256, host-checked)
+    const int co_t = 4 * q4t, g_t = co_t >> gsh;
+    const float inv_lout = 1.0f / (float)a.lout;
+    f32x4 gw_t = {0.f, 0.f, 0.f, 0.f}, gb_t = gw_t, cv0_t = gw_t, cv1_t = gw_t;
+    auto epi_setup = [&]() {  // after s_chan is visible
+        if (epi != UEPI_BIAS) {
+            gw_t = *reinterpret_cast<const f32x4 *>(s_chan + co_t);
+            gb_t = *reinterpret_cast<const f32x4 *>(s_chan + a.coutp + co_t);
+            cv0_t = *reinterpret_cast<const f32x4 *>(s_chan + 2 * a.coutp + co_t);
+            cv1_t = *reinterpret_cast<const f32x4 *>(s_chan + 3 * a.coutp + co_t);
+        }
+    };
     auto epilogue = [&](int64_t r0, int nrow) {
-        const int n_out = nrow * a.lout * cq;
+        const int n_ro = nrow * a.lout;
         constexpr int EU = 4;  // items per thread with their residual loads in flight together
-        for (int i0 = tid; i0 < n_out; i0 += EU * MT) {
+        for (int i0 = tid < tps * cq ? tid / cq : n_ro; i0 < n_ro; i0 += EU * tps) {
             f32x4 rv[EU];
-            int rr[EU], ro_[EU], cc_[EU];
+            int rr[EU], oo_[EU];
 #pragma unroll
             for (int u = 0; u < EU; ++u) {
-                const int i = min(i0 + u * MT, n_out - 1);  // clamped: a duplicate item is recomputed, not stored
-                int q4, oo;
-                const int ro = qdiv(i, cq, inv_cq, q4);
-                rr[u] = qdiv(ro, a.lout, inv_lout, oo);
-                ro_[u] = oo;
-                cc_[u] = 4 * q4;
+                const int ro = min(i0 + u * tps, n_ro - 1);  // clamped: a duplicate item is recomputed, not stored
+                rr[u] = qdiv(ro, a.lout, inv_lout, oo_[u]);
                 if (epi == UEPI_GN_MISH_RES)
-                    rv[u] = ldg4(a.res + ((size_t)(r0 + rr[u]) * a.lout + oo) * a.cout + cc_[u]);
+                    rv[u] = ldg4(a.res + ((size_t)(r0 + rr[u]) * a.lout + oo_[u]) * a.cout + co_t);
             }
 #pragma unroll
             for (int u = 0; u < EU; ++u) {
-                if (i0 + u * MT >= n_out) break;
-                const int r = rr[u], oo = ro_[u], co = cc_[u];
-                const f32x4 raw = *reinterpret_cast<const f32x4 *>(s_out + (size_t)colof(r, oo) * sout + co);
+                if (i0 + u * tps >= n_ro) break;
+                const int r = rr[u], oo = oo_[u];
+                const f32x4 raw = *reinterpret_cast<const f32x4 *>(s_out + (size_t)colof(r, oo) * sout + co_t);
                 const int64_t grow = r0 + r;
                 f32x4 v = raw;
                 if (epi != UEPI_BIAS) {
-                    const int g = co >> gsh;
-                    const float mean = s_stat[2 * (r * a.groups + g)], rstd = s_stat[2 * (r * a.groups + g) + 1];
-                    const f32x4 gw = *reinterpret_cast<const f32x4 *>(s_chan + co);
-                    const f32x4 gb = *reinterpret_cast<const f32x4 *>(s_chan + a.coutp + co);
+                    const float mean = s_stat[2 * (r * a.groups + g_t)], rstd = s_stat[2 * (r * a.groups + g_t) + 1];
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        const float scale = rstd * gw[e];
-                        const float shift = -scale * mean + gb[e];
+                        const float scale = rstd * gw_t[e];
+                        const float shift = -scale * mean + gb_t[e];
                         v[e] = mish(raw[e] * scale + shift);
                     }
                     if (epi == UEPI_GN_MISH_COND) {  // row < b_cand: context branch; else the masked (CFG) branch
                         int64_t cand = grow, br = 0;  // branch = row / b_cand (0: context, 1: masked)
                         while (cand >= a.b_cand) { cand -= a.b_cand; ++br; }
-                        f32x4 cv = *reinterpret_cast<const f32x4 *>(s_chan + (br == 0 ? 2 : 3) * a.coutp + co);
+                        f32x4 cv = br == 0 ? cv0_t : cv1_t;
                         if (a.cp && a.cp_stride && br == 0)
-                            cv = cv + *reinterpret_cast<const f32x4 *>(a.cp + (size_t)cand * a.cp_stride + co);
+                            cv = cv + *reinterpret_cast<const f32x4 *>(a.cp + (size_t)cand * a.cp_stride + co_t);
                         v = v + cv;
                     }
                     if (epi == UEPI_GN_MISH_RES) v = v + rv[u];
                 }
-                float *dst = a.out + ((size_t)grow * a.lout + oo) * a.cout + co;
+                float *dst = a.out + ((size_t)grow * a.lout + oo) * a.cout + co_t;
                 if ((a.cout & 3) == 0) {
                     *reinterpret_cast<f32x4 *>(dst) = v;
                 } else {
-                    for (int e = 0; e < 4 && co + e < a.cout; ++e) dst[e] = v[e];
+                    for (int e = 0; e < 4 && co_t + e < a.cout; ++e) dst[e] = v[e];
                 }
             }
         }
@@ -498,24 +509,27 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
     if constexpr (!PERS) {
         const int64_t r0 = (int64_t)blockIdx.x * a.rb;
         const int nrow = (int)min((int64_t)a.rb, a.rows - r0);
-        stage_direct(r0, nrow);
+        if (!(a.skip & 1)) stage_direct(r0, nrow);
         __syncthreads();
-        if (a.alias) {  // one job per wave (host-checked): finish every read of the staged input first
-            if (wave < jobs) compute(wave);
-            __syncthreads();
-            if (wave < jobs) store(wave);
-        } else {
-            for (int job = wave; job < jobs; job += MT / 64) {
-                compute(job);
-                store(job);
+        epi_setup();
+        if (!(a.skip & 2)) {
+            if (a.alias) {  // one job per wave (host-checked): finish every read of the staged input first
+                if (wave < jobs) compute(wave);
+                __syncthreads();
+                if (wave < jobs) store(wave);
+            } else {
+                for (int job = wave; job < jobs; job += MT / 64) {
+                    compute(job);
+                    store(job);
+                }
             }
         }
         __syncthreads();
-        if (epi != UEPI_BIAS) {
+        if (epi != UEPI_BIAS && !(a.skip & 4)) {
             stats(nrow);
             __syncthreads();
         }
-        epilogue(r0, nrow);
+        if (!(a.skip & 8)) epilogue(r0, nrow);
     } else {  // host: no alias, 16-byte staging, items per thread <= SUP
         int64_t blk = blockIdx.x;
         {
@@ -524,6 +538,7 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
             stage_commit();
         }
         __syncthreads();
+        epi_setup();
         for (; blk < nblocks; blk += gridDim.x) {
             const int64_t r0 = blk * a.rb;
             const int nrow = (int)min((int64_t)a.rb, a.rows - r0);
@@ -844,5 +859,11 @@ hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::
         std::lock_guard<std::mutex> g(g_mx_mu);
         g_mx_cache[key] = pick;
     }
+    static const int skip = [] {  // experiment knob: skip kernel phases (results are garbage)
+        const char *e = getenv("MPCD_UNET_SKIP");
+        return e ? atoi(e) : 0;
+    }();
+    k.skip = skip;
+    if (skip) pick = cands[0].pers ? cands[1] : cands[0];
     return launch_choice(kind, planes, k, pick, st);
 }
