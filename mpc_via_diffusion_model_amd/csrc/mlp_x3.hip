@@ -30,8 +30,18 @@ namespace {
 using namespace mlpc;
 
 constexpr int ROWS = 32;
-constexpr int THREADS = 256;
-enum { SPLIT = 0, PAIRED = 1 };
+// WAVES = 8 (two per SIMD): while one wave of a SIMD waits on a barrier, an LDS read or its own
+// MFMA chain, the other issues, and a bf16 MFMA leaves vector issue free for 8 of its 16 cycles, so
+// one wave's Mish / split VALU runs under the other's MFMAs. Hidden layers then map as PAIR8
+// (N = 128: wave w -> n-tile w, both column tiles) or WIDE8 (N <= 64: wave w -> column tile w >> 2,
+// n-tiles (w & 3) + 4j); the final layer, which pairs a candidate's two CFG rows, runs on waves 0-3
+// in the PAIRED form. WAVES = 4 keeps the one-wave-per-SIMD schedule (hidden()).
+#ifndef MPCD_X3_WAVES
+#define MPCD_X3_WAVES 8
+#endif
+constexpr int THREADS = 64 * MPCD_X3_WAVES;
+constexpr int WAVES = THREADS / 64;
+enum { SPLIT = 0, PAIRED = 1, WIDE8 = 2, PAIR8 = 3 };
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -99,7 +109,7 @@ struct Lds3 {
 };
 
 template <int N>
-constexpr int mode_for() { return N == 32 ? SPLIT : PAIRED; }
+constexpr int mode_for() { return WAVES == 8 ? (N >= 128 ? PAIR8 : WIDE8) : N == 32 ? SPLIT : PAIRED; }
 
 constexpr int epi_of(int l) { return l == 12 ? EPI_NONE : (l % 2 == 1) ? EPI_CMISH : EPI_MISH; }
 
@@ -108,7 +118,7 @@ constexpr int epi_of(int l) { return l == 12 ? EPI_NONE : (l % 2 == 1) ? EPI_CMI
 template <int K, int N, int MODE>
 struct WFrag3 {
     static constexpr int NT = N / 16;
-    static constexpr int T = MODE == SPLIT ? NT / 2 : (NT + 3) / 4;
+    static constexpr int T = MODE == SPLIT ? NT / 2 : MODE == PAIR8 ? (NT + 7) / 8 : (NT + 3) / 4;  // n-tiles per wave
     static constexpr int KC = K / 32;
     u32x4 v[T][KC][3];
 };
@@ -116,7 +126,7 @@ struct WFrag3 {
 template <int K, int N, int MODE>
 MPCD_DEV int ntile_of(int wave, int j)
 {
-    return MODE == SPLIT ? (wave >> 1) + 2 * j : wave + 4 * j;
+    return MODE == SPLIT ? (wave >> 1) + 2 * j : MODE == PAIR8 ? wave + 8 * j : (wave & 3) + 4 * j;
 }
 
 // One wave-uniform buffer descriptor per layer; chunk (nt, kc, plane) at soffset ((nt*KC+kc)*3+p) KiB.
@@ -131,8 +141,9 @@ MPCD_DEV void load_w3(WFrag3<K, N, MODE> &f, const float *__restrict__ wp, int w
         (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(3 * K * N * 2), 0x00020000);
 #pragma unroll
     for (int j = 0; j < F::T; ++j) {
-        const int nt = ntile_of<K, N, MODE>(wave, j);
-        if (MODE == PAIRED && NT % 4 != 0 && nt >= NT) continue;
+        // clamped, not skipped: the load count stays path-independent (a skipped load makes the
+        // compiler drain vmcnt(0)); a wave with no tile n uses nothing it loaded
+        const int nt = min(ntile_of<K, N, MODE>(wave, j), NT - 1);
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
@@ -263,6 +274,87 @@ struct MlpX3 {
             __builtin_amdgcn_sched_barrier(0);
         }
         group(G - 1, true);
+    }
+
+    // Hidden layer l on 8 waves (PAIR8 / WIDE8 above). Activation fragments are read one k-chunk
+    // ahead rather than all up front (the partner wave covers the LDS latency), which keeps the
+    // register budget of two waves per SIMD.
+    template <int l>
+    static MPCD_DEV void hidden8(const WFrag3<A::K[l], A::N[l], mode_for<A::N[l]>()> &f, char *lds, int wave, int lane)
+    {
+        constexpr int K = A::K[l], N = A::N[l], MODE = mode_for<N>(), EPI = epi_of(l);
+        using F = WFrag3<K, N, MODE>;
+        constexpr int T = F::T, KC = F::KC, NT = N / 16;
+        constexpr int NCT = MODE == PAIR8 ? 2 : 1;
+        static_assert(MODE == PAIR8 || MODE == WIDE8, "8-wave layer modes");
+        const int col = lane & 15, q = lane >> 4;
+        const bool in_shared = l == 0 && NB == 2;  // CFG: both branches read the candidate's x
+        auto ct_of = [&](int c) { return MODE == PAIR8 ? c : (wave >> 2); };
+        bool ok[T];
+#pragma unroll
+        for (int j = 0; j < T; ++j) ok[j] = ntile_of<K, N, MODE>(wave, j) < NT;
+        f32x4 acc[T][NCT];
+#pragma unroll
+        for (int c = 0; c < NCT; ++c) {
+            const int ct = ct_of(c);
+            const float *init = reinterpret_cast<const float *>(
+                lds + (EPI == EPI_CMISH ? ((NB == 2 && ct == 1) ? L::TPU : L::TPC) + cond_off(l / 2) * 4
+                                        : L::BI + A::boff(l) * 4));
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+                acc[j][c] = *reinterpret_cast<const f32x4 *>(init + min(ntile_of<K, N, MODE>(wave, j), NT - 1) * 16 + 4 * q);
+        }
+        auto ldx = [&](u32x4 (&x)[NCT][3], int kc) {
+#pragma unroll
+            for (int c = 0; c < NCT; ++c) {
+                const int row = in_shared ? col : ct_of(c) * 16 + col;
+                load_x3(x[c], lds + L::in_off(l) + row * L::in_rs(l) + (kc * 32 + 8 * q) * 2, L::in_pl(l));
+            }
+        };
+        u32x4 xc[NCT][3], xn[NCT][3];
+        ldx(xc, 0);
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+            if (kc + 1 < KC) ldx(xn, kc + 1);
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+                if (ok[j])
+#pragma unroll
+                    for (int c = 0; c < NCT; ++c) acc[j][c] = mfma_x3(f.v[j][kc], xc[c], acc[j][c]);
+            if (kc + 1 < KC)
+#pragma unroll
+                for (int c = 0; c < NCT; ++c)
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl) xc[c][pl] = xn[c][pl];
+        }
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            if (!ok[j]) continue;
+            const int n = ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q;
+#pragma unroll
+            for (int c = 0; c < NCT; ++c) {
+                f32x4 v = acc[j][c];
+                if (EPI != EPI_NONE) {
+                    v.x = mish(v.x);
+                    v.y = mish(v.y);
+                    v.z = mish(v.z);
+                    v.w = mish(v.w);
+                }
+                u32x2 p0, p1, p2;
+                split3(v, p0, p1, p2);
+                char *o = lds + L::out_off(l) + (ct_of(c) * 16 + col) * L::out_rs(l) + n * 2;
+                *reinterpret_cast<u32x2 *>(o) = p0;
+                *reinterpret_cast<u32x2 *>(o + L::out_pl(l)) = p1;
+                *reinterpret_cast<u32x2 *>(o + 2 * L::out_pl(l)) = p2;
+            }
+        }
+    }
+
+    template <int l>
+    static MPCD_DEV void layer(const WFrag3<A::K[l], A::N[l], mode_for<A::N[l]>()> &f, char *lds, int wave, int lane)
+    {
+        if constexpr (WAVES == 8) hidden8<l>(f, lds, wave, lane);
+        else hidden<l>(f, lds, wave, lane);
     }
 
     // x (4 features) -> fp32 row in XB and the three bf16 planes layer 0 reads
@@ -416,7 +508,7 @@ struct MlpX3 {
         load_w3(w0, W(0), wave, lane16);
         f32x4 nz[NZT][NB];
         StepPlan sp = load_plan(p.plan, 0);
-        fetch_noise(nz, p, sp, 0, cand0, wave, lane);
+        if (wave < 4) fetch_noise(nz, p, sp, 0, cand0, wave, lane);
         const int tpi = threadIdx.x < COND_TOTAL / 4 ? (int)threadIdx.x : 0;
         f32x4 tpre = reinterpret_cast<const f32x4 *>(p.tproj)[tpi];
 
@@ -449,55 +541,55 @@ struct MlpX3 {
                 reinterpret_cast<f32x4 *>(lds + L::TPC)[tpi] = u + reinterpret_cast<const f32x4 *>(lds + L::CPS)[tpi];
             }
             tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 1 < p.n_steps ? s + 1 : s) * COND_TOTAL)[tpi];
-            hidden<0>(w0, lds, wave, lane);
+            layer<0>(w0, lds, wave, lane);
             WFrag3<A::K[2], A::N[2], mode_for<A::N[2]>()> w2;
             load_w3(w2, W(2), wave, lane16);
             bar(1);
-            hidden<1>(w1, lds, wave, lane);
+            layer<1>(w1, lds, wave, lane);
             WFrag3<A::K[3], A::N[3], mode_for<A::N[3]>()> w3;
             load_w3(w3, W(3), wave, lane16);
             bar(2);
-            hidden<2>(w2, lds, wave, lane);
+            layer<2>(w2, lds, wave, lane);
             WFrag3<A::K[4], A::N[4], mode_for<A::N[4]>()> w4;
             load_w3(w4, W(4), wave, lane16);
             bar(3);
-            hidden<3>(w3, lds, wave, lane);
+            layer<3>(w3, lds, wave, lane);
             WFrag3<A::K[5], A::N[5], mode_for<A::N[5]>()> w5;
             load_w3(w5, W(5), wave, lane16);
             bar(4);
-            hidden<4>(w4, lds, wave, lane);
+            layer<4>(w4, lds, wave, lane);
             WFrag3<A::K[6], A::N[6], mode_for<A::N[6]>()> w6;
             load_w3(w6, W(6), wave, lane16);
             bar(5);
-            hidden<5>(w5, lds, wave, lane);
+            layer<5>(w5, lds, wave, lane);
             WFrag3<A::K[7], A::N[7], mode_for<A::N[7]>()> w7;
             load_w3(w7, W(7), wave, lane16);
             bar(6);
-            hidden<6>(w6, lds, wave, lane);
+            layer<6>(w6, lds, wave, lane);
             WFrag3<A::K[8], A::N[8], mode_for<A::N[8]>()> w8;
             load_w3(w8, W(8), wave, lane16);
             bar(7);
-            hidden<7>(w7, lds, wave, lane);
+            layer<7>(w7, lds, wave, lane);
             WFrag3<A::K[9], A::N[9], mode_for<A::N[9]>()> w9;
             load_w3(w9, W(9), wave, lane16);
             bar(8);
-            hidden<8>(w8, lds, wave, lane);
+            layer<8>(w8, lds, wave, lane);
             WFrag3<A::K[10], A::N[10], mode_for<A::N[10]>()> w10;
             load_w3(w10, W(10), wave, lane16);
             bar(9);
-            hidden<9>(w9, lds, wave, lane);
+            layer<9>(w9, lds, wave, lane);
             WFrag3<A::K[11], A::N[11], mode_for<A::N[11]>()> w11;
             load_w3(w11, W(11), wave, lane16);
             bar(10);
-            hidden<10>(w10, lds, wave, lane);
+            layer<10>(w10, lds, wave, lane);
             WFrag3<A::K[12], A::N[12], mode_for<A::N[12]>()> w12;
             load_w3(w12, W(12), wave, lane16);
             bar(11);
-            hidden<11>(w11, lds, wave, lane);
+            layer<11>(w11, lds, wave, lane);
             FW w13;
             load_w3(w13, W(13), wave, lane16);
             bar(12);
-            hidden<12>(w12, lds, wave, lane);
+            layer<12>(w12, lds, wave, lane);
             const StepPlan cur = sp;
             f32x4 nzc[NZT][NB];
 #pragma unroll
@@ -506,12 +598,12 @@ struct MlpX3 {
                 for (int g = 0; g < NB; ++g) nzc[j][g] = nz[j][g];
             if (s + 1 < p.n_steps) {
                 sp = load_plan(p.plan, s + 1);
-                fetch_noise(nz, p, sp, s + 1, cand0, wave, lane);
+                if (wave < 4) fetch_noise(nz, p, sp, s + 1, cand0, wave, lane);
             }
             // next step's layer-0 weights; unconditional (a path-dependent load count drains vmcnt(0))
             load_w3(w0, W(0), wave, lane16);
             bar(13);
-            final_and_update(w13, lds, p, cur, s, cand0, nzc, wave, lane);
+            if (wave < 4) final_and_update(w13, lds, p, cur, s, cand0, nzc, wave, lane);
         }
 #ifdef MPCD_PROF_LAYERS
         {
