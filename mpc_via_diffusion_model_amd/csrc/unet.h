@@ -51,6 +51,12 @@ struct ConvMK {
     int stat_off;           // LDS byte offset of the GroupNorm statistics (then the per-channel table)
     int cpg_shift;          // log2(cout / groups)
     int skip;               // experiment only (MPCD_UNET_SKIP): bit 0 staging, 1 GEMM, 2 statistics, 3 epilogue
+    // LDS placement (set by unet_launch_mx / unet_launch_mx_rtb): staged input planes and fp32 tile
+    int in_off, out_off;
+    // fused ResidualTemporalBlock, first conv only: the epilogue writes its result as the second
+    // conv's staged planes (LDS offset nx_off, per-position stride nx_cs, window nx_win, left halo
+    // nx_halo_l) instead of storing it to HBM
+    int lds_out, nx_off, nx_cs, nx_win, nx_halo_l;
 };
 
 struct UnetWeights {
@@ -92,6 +98,11 @@ void unet_pack_mx(int kind, int cin, int cout, int planes, const float *w_host, 
                   std::vector<uint16_t> &pack);
 // Choose rows per workgroup / tile shape and launch; kind = UCONV_*, planes 1 or 3.
 hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::string *why);
+
+// A ResidualTemporalBlock's two 5-tap convs (k1: conv1 + GN/Mish/cond -> k1.out; k2: conv2 + GN/Mish
+// + residual, k2.xa = k1.out) as one fused launch when that measures faster than the pair (the
+// intermediate then stays in LDS and k1.out is not written). MPCD_UNET_FUSE=0/1 forces either form.
+hipError_t unet_launch_mx_rtb(int planes, ConvMK &k1, ConvMK &k2, hipStream_t st, std::string *why);
 
 using TensorLookup = std::function<const float *(const char *)>;
 

@@ -601,6 +601,38 @@ hipError_t dispatch(int kind, int epi, const ConvK &k, size_t lds, hipStream_t s
     return hipErrorInvalidValue;
 }
 
+// launch parameters of one mx conv (bf16 / f16 MFMA family)
+ConvMK make_mk(const Ctx &c, const ConvLayer &L, int epi, const float *xa, int ca, const float *xb, int cb,
+               int64_t x_rows, int lin, const float *res, float *out)
+{
+    ConvMK k{};
+    k.xa = xa;
+    k.xb = xb;
+    k.ca = ca;
+    k.cb = cb;
+    k.cinp = L.cinp8;
+    k.kc = L.kc;
+    k.x_rows = x_rows;
+    k.w = L.wmx;
+    k.bias = L.bias;
+    k.gn_w = L.gn_w;
+    k.gn_b = L.gn_b;
+    k.groups = L.groups;
+    k.tp = L.cond_off >= 0 ? c.tp + L.cond_off : nullptr;
+    k.cp = (L.cond_off >= 0 && c.cp) ? c.cp + L.cond_off : nullptr;
+    k.cp_stride = c.cp_stride;
+    k.b_cand = c.b_cand;
+    k.res = res;
+    k.out = out;
+    k.rows = c.rows;
+    k.lin = lin;
+    k.lout = L.kind == CONV_DOWN3 ? lin / 2 : L.kind == CONV_UP4 ? lin * 2 : lin;
+    k.cout = L.cout;
+    k.coutp = L.coutp;
+    k.epi = epi;
+    return k;
+}
+
 // out = layer(xa [, xb]); lin = input length
 int run_conv(Ctx &c, int epi, const float *xa, int ca, const float *xb, int cb, int64_t x_rows, int lin,
              const float *res, float *out)
@@ -608,31 +640,7 @@ int run_conv(Ctx &c, int epi, const float *xa, int ca, const float *xb, int cb, 
     const ConvLayer &L = c.W->layers[c.li++];
     if (L.cin != ca + cb) return uerr(MPCD_EINVAL, "UNet plan: channel mismatch");
     if (c.W->planes) {
-        ConvMK k{};
-        k.xa = xa;
-        k.xb = xb;
-        k.ca = ca;
-        k.cb = cb;
-        k.cinp = L.cinp8;
-        k.kc = L.kc;
-        k.x_rows = x_rows;
-        k.w = L.wmx;
-        k.bias = L.bias;
-        k.gn_w = L.gn_w;
-        k.gn_b = L.gn_b;
-        k.groups = L.groups;
-        k.tp = L.cond_off >= 0 ? c.tp + L.cond_off : nullptr;
-        k.cp = (L.cond_off >= 0 && c.cp) ? c.cp + L.cond_off : nullptr;
-        k.cp_stride = c.cp_stride;
-        k.b_cand = c.b_cand;
-        k.res = res;
-        k.out = out;
-        k.rows = c.rows;
-        k.lin = lin;
-        k.lout = L.kind == CONV_DOWN3 ? lin / 2 : L.kind == CONV_UP4 ? lin * 2 : lin;
-        k.cout = L.cout;
-        k.coutp = L.coutp;
-        k.epi = epi;
+        ConvMK k = make_mk(c, L, epi, xa, ca, xb, cb, x_rows, lin, res, out);
         if (epi == EPI_GN_MISH_COND && !k.tp) return uerr(MPCD_EINVAL, "UNet plan: missing cond");
         if (L.cout % L.groups != 0) return uerr(MPCD_EUNSUP, "UNet: cout not divisible by groups");
         std::string why;
@@ -692,6 +700,32 @@ int run_rtb(Ctx &c, Buffers &B, const float *xa, int ca, const float *xb, int cb
             float *tmp_h, float *tmp_r, float *out)
 {
     int rc;
+    if (c.W->planes) {  // mx family: [residual 1x1 conv], then conv1 + conv2 (fused when that measures faster)
+        const ConvLayer &L1 = c.W->layers[c.li];
+        const bool has_res = ca + cb != cout;
+        const ConvLayer &L2 = c.W->layers[c.li + (has_res ? 2 : 1)];
+        if (L1.cin != ca + cb || L2.cin != cout || L1.cout != cout || L2.cout != cout)
+            return uerr(MPCD_EINVAL, "UNet plan: channel mismatch");
+        const float *res = xa;
+        if (has_res) {
+            c.li += 1;
+            if ((rc = run_conv(c, EPI_BIAS, xa, ca, xb, cb, x_rows, L, nullptr, tmp_r))) return rc;
+            c.li -= 2;
+            res = tmp_r;
+        } else if (x_rows != c.rows) {
+            return uerr(MPCD_EUNSUP, "UNet: identity residual on shared input");
+        }
+        ConvMK k1 = make_mk(c, L1, EPI_GN_MISH_COND, xa, ca, xb, cb, x_rows, L, nullptr, tmp_h);
+        ConvMK k2 = make_mk(c, L2, EPI_GN_MISH_RES, tmp_h, cout, nullptr, 0, c.rows, L, res, out);
+        c.li += has_res ? 3 : 2;
+        if (!k1.tp) return uerr(MPCD_EINVAL, "UNet plan: missing cond");
+        if (L1.cout % L1.groups != 0 || L2.cout % L2.groups != 0)
+            return uerr(MPCD_EUNSUP, "UNet: cout not divisible by groups");
+        std::string why;
+        hipError_t e = unet_launch_mx_rtb(c.W->planes, k1, k2, c.st, &why);
+        if (e != hipSuccess) return uerr(MPCD_EHIP, "mx block launch: " + (why.empty() ? hipGetErrorString(e) : why));
+        return MPCD_OK;
+    }
     if ((rc = run_conv(c, EPI_GN_MISH_COND, xa, ca, xb, cb, x_rows, L, nullptr, tmp_h))) return rc;
     const float *res = xa;
     if (ca + cb != cout) {

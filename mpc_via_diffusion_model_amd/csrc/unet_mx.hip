@@ -25,6 +25,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -42,6 +43,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int MT = 256;  // threads per workgroup
 
@@ -143,12 +145,53 @@ struct KWalk {
 // area once b's GEMM has finished reading it.
 constexpr int SUP = 6;  // staging items per thread a persistent workgroup keeps in flight (host-checked)
 
-template <int KIND, int P, int NN, int NC, bool PERS>
-__global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
+// 4 fp32 -> P planes of 4 values (8 bytes each)
+template <int P>
+MPCD_DEV void split4(const f32x4 &v, u32x2 (&o)[P])
+{
+    if constexpr (P == 1) {
+        o[0] = u32x2{pk_f16(v.x, v.y), pk_f16(v.z, v.w)};
+    } else {
+        const uint32_t a0 = pk_bf16(v.x, v.y), a1 = pk_bf16(v.z, v.w);
+        const f32x4 r = v - f32x4{bf_lo(a0), bf_hi(a0), bf_lo(a1), bf_hi(a1)};
+        const uint32_t b0 = pk_bf16(r.x, r.y), b1 = pk_bf16(r.z, r.w);
+        const f32x4 t = r - f32x4{bf_lo(b0), bf_hi(b0), bf_lo(b1), bf_hi(b1)};
+        o[0] = u32x2{a0, a1};
+        o[1] = u32x2{b0, b1};
+        o[2] = u32x2{pk_bf16(t.x, t.y), pk_bf16(t.z, t.w)};
+    }
+}
+
+// The launch's convs: one (NPH = 1), or a ResidualTemporalBlock's two 5-tap convs (NPH = 2): the
+// first conv's GroupNorm / Mish / cond epilogue writes its rows straight into the second conv's
+// staged planes in LDS (same values the unfused pair would store to HBM and re-stage, so the
+// results are bit-identical), and only the block output goes back to HBM.
+struct ConvMK2 {
+    ConvMK ph[2];
+};
+
+template <int KIND, int P, int NN, int NC, bool PERS, int NPH>
+__global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
 {
     extern __shared__ __attribute__((aligned(16))) char sm[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    static_assert(NPH == 1 || (!PERS && KIND == UCONV_SAME5), "fused pairs: 5-tap convs, one row block per workgroup");
+    if constexpr (NPH == 2) {  // zero the halo positions of the second conv's staging window (rows rb)
+        const ConvMK &a = as.ph[0];
+        const int hp = a.nx_win - a.lout, u16 = a.nx_cs >> 4;  // halo positions per row, 16-B units per position
+        const int nrowB = a.nx_win * a.nx_cs, nplaneB = a.rb * nrowB;
+        const int n = P * a.rb * hp * u16;
+        for (int i = tid; i < n; i += MT) {
+            const int u = i % u16, t = i / u16, h = t % hp, rp = t / hp, r = rp % a.rb, pl = rp / a.rb;
+            const int pos = h < a.nx_halo_l ? h : a.lout + h;
+            *reinterpret_cast<u32x4 *>(sm + a.nx_off + pl * nplaneB + r * nrowB + pos * a.nx_cs + u * 16) =
+                u32x4{0u, 0u, 0u, 0u};
+        }
+    }
+#pragma unroll
+    for (int ph = 0; ph < NPH; ++ph) {
+    const ConvMK &a = as.ph[ph];
     const int win = a.lin + a.halo_l + a.halo_r;
     const int rowB = win * a.cs, planeB = a.rb * rowB;
     const int64_t nblocks = (a.rows + a.rb - 1) / a.rb;
@@ -199,7 +242,7 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
         u32x4 o[P];
         split8<P>(lo, hi, o);
 #pragma unroll
-        for (int pl = 0; pl < P; ++pl) *reinterpret_cast<u32x4 *>(sm + pl * planeB + dst) = o[pl];
+        for (int pl = 0; pl < P; ++pl) *reinterpret_cast<u32x4 *>(sm + a.in_off + pl * planeB + dst) = o[pl];
     };
     auto stage_direct = [&](int64_t r0, int nrow) {
         if ((a.ca & 7) == 0 && (a.cb & 7) == 0) {
@@ -271,7 +314,7 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
     const int jobs = npj * ncg * npar;
     const int col = lane & 15, q = lane >> 4;
     const int sout = a.coutp + 4;
-    float *s_out = reinterpret_cast<float *>(a.alias ? sm : sm + P * planeB);
+    float *s_out = reinterpret_cast<float *>(sm + a.out_off);
 
     const uint64_t wa = (uint64_t)a.w;
     const uint32_t wlo = __builtin_amdgcn_readfirstlane((uint32_t)wa), whi = __builtin_amdgcn_readfirstlane((uint32_t)(wa >> 32));
@@ -327,7 +370,7 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
             for (int cc = 0; cc < NC; ++cc)
 #pragma unroll
                 for (int pl = 0; pl < P; ++pl)
-                    B[cc][pl] = *reinterpret_cast<const u32x4 *>(sm + pl * planeB + bb[cc] + koff);
+                    B[cc][pl] = *reinterpret_cast<const u32x4 *>(sm + a.in_off + pl * planeB + bb[cc] + koff);
         };
         auto mmas = [&](const u32x4 (&A)[NN][P], const u32x4 (&B)[NC][P]) {
 #pragma unroll
@@ -496,6 +539,15 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
                     }
                     if (epi == UEPI_GN_MISH_RES) v = v + rv[u];
                 }
+                if (NPH == 2 && ph == 0) {  // the second conv's staged planes (cout % 4 == 0, host-checked)
+                    u32x2 o[P];
+                    split4<P>(v, o);
+                    const int nrowB = a.nx_win * a.nx_cs;
+                    char *d = sm + a.nx_off + r * nrowB + (oo + a.nx_halo_l) * a.nx_cs + co_t * 2;
+#pragma unroll
+                    for (int pl = 0; pl < P; ++pl) *reinterpret_cast<u32x2 *>(d + pl * a.rb * nrowB) = o[pl];
+                    continue;
+                }
                 float *dst = a.out + ((size_t)grow * a.lout + oo) * a.cout + co_t;
                 if ((a.cout & 3) == 0) {
                     *reinterpret_cast<f32x4 *>(dst) = v;
@@ -509,7 +561,7 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
     if constexpr (!PERS) {
         const int64_t r0 = (int64_t)blockIdx.x * a.rb;
         const int nrow = (int)min((int64_t)a.rb, a.rows - r0);
-        if (!(a.skip & 1)) stage_direct(r0, nrow);
+        if (ph == 0 && !(a.skip & 1)) stage_direct(r0, nrow);
         __syncthreads();
         epi_setup();
         if (!(a.skip & 2)) {
@@ -556,6 +608,8 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK a)
             __syncthreads();  // tile and statistics read before the next block overwrites them
         }
     }
+    if (ph + 1 < NPH) __syncthreads();  // the second conv's planes complete; tile / statistics free
+    }
 }
 
 // ---- host side
@@ -594,10 +648,11 @@ constexpr Tile kTiles1[] = {{4, 8}, {2, 8}, {2, 4}, {1, 8}, {1, 4}};
 
 int g_n_cu = 0;  // compute units of the device (persistent grids)
 
-template <int KIND, int P, int NN, int NC, bool PERS>
-hipError_t launch_one(const ConvMK &k, size_t lds, hipStream_t st)
+template <int KIND, int P, int NN, int NC, bool PERS, int NPH = 1>
+hipError_t launch_one(const ConvMK2 &k2, size_t lds, hipStream_t st)
 {
-    auto *fn = reinterpret_cast<const void *>(&conv_mx_kernel<KIND, P, NN, NC, PERS>);
+    const ConvMK &k = k2.ph[0];
+    auto *fn = reinterpret_cast<const void *>(&conv_mx_kernel<KIND, P, NN, NC, PERS, NPH>);
     static bool set = false;
     static int resident = 0;  // workgroups per CU at this kernel's registers and the LDS of its first use
     static size_t resident_lds = 0;
@@ -623,12 +678,12 @@ hipError_t launch_one(const ConvMK &k, size_t lds, hipStream_t st)
         }
         blocks = std::min<int64_t>(blocks, (int64_t)resident * g_n_cu);
     }
-    hipLaunchKernelGGL((conv_mx_kernel<KIND, P, NN, NC, PERS>), dim3((unsigned)blocks), dim3(MT), lds, st, k);
+    hipLaunchKernelGGL((conv_mx_kernel<KIND, P, NN, NC, PERS, NPH>), dim3((unsigned)blocks), dim3(MT), lds, st, k2);
     return hipGetLastError();
 }
 
 template <int KIND, int P>
-hipError_t launch_kind(const ConvMK &k, Tile t, bool pers, size_t lds, hipStream_t st)
+hipError_t launch_kind(const ConvMK2 &k, Tile t, bool pers, size_t lds, hipStream_t st)
 {
 #define T_(A, B)                                                                          \
     if (t.nn == A && t.nc == B)                                                           \
@@ -678,16 +733,55 @@ hipError_t launch_choice(int kind, int planes, ConvMK &k, const MxChoice &ch, hi
     k.rb = ch.rb;
     k.alias = ch.alias;
     k.stat_off = ch.stat_off;
+    k.in_off = 0;
+    k.out_off = ch.alias ? 0 : planes * ch.rb * (k.lin + k.halo_l + k.halo_r) * k.cs;
+    k.lds_out = 0;
+    ConvMK2 k2{};
+    k2.ph[0] = k;
 #define K_(KD)                                                                        \
     if (kind == KD)                                                                   \
-        return planes == 1 ? launch_kind<KD, 1>(k, ch.t, ch.pers, ch.lds, st)         \
-                           : launch_kind<KD, 3>(k, ch.t, ch.pers, ch.lds, st);
+        return planes == 1 ? launch_kind<KD, 1>(k2, ch.t, ch.pers, ch.lds, st)        \
+                           : launch_kind<KD, 3>(k2, ch.t, ch.pers, ch.lds, st);
     K_(UCONV_SAME5)
     K_(UCONV_DOWN3)
     K_(UCONV_UP4)
     K_(UCONV_PW1)
 #undef K_
     return hipErrorInvalidValue;
+}
+
+hipError_t prep_geom(int kind, ConvMK &k, std::string *why)
+{
+    const int cinp = k.cinp, KC = k.kc;
+    const int T = KC * 32 / cinp;  // taps / slots covered by the padded K (zero weights beyond ks)
+    if (kind == UCONV_SAME5) {
+        k.halo_l = 2;
+        k.halo_r = std::max(2, T - 3);
+    } else if (kind == UCONV_DOWN3) {
+        k.halo_l = 1;
+        k.halo_r = std::max(0, T - 3);
+    } else if (kind == UCONV_UP4) {
+        k.halo_l = std::max(1, T - 1);
+        k.halo_r = 1;
+    } else {
+        k.halo_l = 0;
+        k.halo_r = T - 1;
+    }
+    // per-position stride: an odd number of 16-byte units
+    int cs = cinp * 2;
+    if (((cs / 16) & 1) == 0) cs += 16;
+    k.cs = cs;
+    if (k.epi != UEPI_BIAS) {
+        const int cpg = k.cout / k.groups;
+        int sh = 0;
+        while ((1 << sh) < cpg) ++sh;
+        if ((1 << sh) != cpg || cpg < 4 || k.groups > 32) {
+            if (why) *why = "UNet mx conv: GroupNorm needs a power-of-two group width >= 4 and <= 32 groups";
+            return hipErrorInvalidValue;
+        }
+        k.cpg_shift = sh;
+    }
+    return hipSuccess;
 }
 
 }  // namespace
@@ -738,35 +832,9 @@ void unet_pack_mx(int kind, int cin, int cout, int planes, const float *w_host, 
 
 hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::string *why)
 {
-    const int cinp = k.cinp, KC = k.kc;
-    const int T = KC * 32 / cinp;  // taps / slots covered by the padded K (zero weights beyond ks)
-    if (kind == UCONV_SAME5) {
-        k.halo_l = 2;
-        k.halo_r = std::max(2, T - 3);
-    } else if (kind == UCONV_DOWN3) {
-        k.halo_l = 1;
-        k.halo_r = std::max(0, T - 3);
-    } else if (kind == UCONV_UP4) {
-        k.halo_l = std::max(1, T - 1);
-        k.halo_r = 1;
-    } else {
-        k.halo_l = 0;
-        k.halo_r = T - 1;
-    }
-    // per-position stride: an odd number of 16-byte units
-    int cs = cinp * 2;
-    if (((cs / 16) & 1) == 0) cs += 16;
-    k.cs = cs;
-    if (k.epi != UEPI_BIAS) {
-        const int cpg = k.cout / k.groups;
-        int sh = 0;
-        while ((1 << sh) < cpg) ++sh;
-        if ((1 << sh) != cpg || cpg < 4 || k.groups > 32) {
-            if (why) *why = "UNet mx conv: GroupNorm needs a power-of-two group width >= 4 and <= 32 groups";
-            return hipErrorInvalidValue;
-        }
-        k.cpg_shift = sh;
-    }
+    hipError_t ge = prep_geom(kind, k, why);
+    if (ge != hipSuccess) return ge;
+    const int KC = k.kc, cs = k.cs, cinp = k.cinp;
     const int win = k.lin + k.halo_l + k.halo_r;
     const int NT = k.coutp / 16, npar = kind == UCONV_UP4 ? 2 : 1;
     const int nprod = planes == 1 ? 1 : 6;
@@ -866,4 +934,169 @@ hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::
     k.skip = skip;
     if (skip) pick = cands[0].pers ? cands[1] : cands[0];
     return launch_choice(kind, planes, k, pick, st);
+}
+
+// ---- fused ResidualTemporalBlock (NPH = 2)
+
+namespace {
+
+struct RtbChoice {
+    int fused;  // 0: the two convs as separate launches (their own measured picks)
+    int rb;
+    Tile t;
+    size_t lds;
+    int x_off;     // LDS byte offset of the second conv's staged planes
+    int stat_off;  // LDS byte offset of the statistics / per-channel table
+    double model;
+};
+
+struct RtbKey {
+    MxKey a, b;
+    bool operator<(const RtbKey &o) const { return a < o.a || (!(o.a < a) && b < o.b); }
+};
+std::map<RtbKey, RtbChoice> g_rtb_cache;
+
+template <int P>
+hipError_t launch_fused(const ConvMK2 &k2, Tile t, size_t lds, hipStream_t st)
+{
+#define T_(A, B) \
+    if (t.nn == A && t.nc == B) return launch_one<UCONV_SAME5, P, A, B, false, 2>(k2, lds, st);
+    if constexpr (P == 3) {
+        T_(2, 4) T_(1, 8) T_(1, 4)
+    } else {
+        T_(4, 8) T_(2, 8) T_(2, 4) T_(1, 8) T_(1, 4)
+    }
+#undef T_
+    return hipErrorInvalidValue;
+}
+
+// LDS: [first conv's staged planes | its fp32 tile] (the second conv's fp32 tile reuses the start),
+// then the second conv's staged planes at x_off, then the statistics / per-channel table.
+hipError_t launch_rtb_choice(int planes, const ConvMK &k1, const ConvMK &k2, const RtbChoice &ch, hipStream_t st)
+{
+    ConvMK2 kk{};
+    kk.ph[0] = k1;
+    kk.ph[1] = k2;
+    for (int i = 0; i < 2; ++i) {
+        ConvMK &k = kk.ph[i];
+        k.rb = ch.rb;
+        k.alias = 0;
+        k.stat_off = ch.stat_off;
+        k.lds_out = i == 0;
+    }
+    kk.ph[0].in_off = 0;
+    kk.ph[0].out_off = planes * ch.rb * (k1.lin + k1.halo_l + k1.halo_r) * k1.cs;
+    kk.ph[0].nx_off = ch.x_off;
+    kk.ph[0].nx_cs = k2.cs;
+    kk.ph[0].nx_win = k2.lin + k2.halo_l + k2.halo_r;
+    kk.ph[0].nx_halo_l = k2.halo_l;
+    kk.ph[1].in_off = ch.x_off;
+    kk.ph[1].out_off = 0;
+    return planes == 1 ? launch_fused<1>(kk, ch.t, ch.lds, st) : launch_fused<3>(kk, ch.t, ch.lds, st);
+}
+
+}  // namespace
+
+hipError_t unet_launch_mx_rtb(int planes, ConvMK &k1, ConvMK &k2, hipStream_t st, std::string *why)
+{
+    auto unfused = [&]() -> hipError_t {
+        hipError_t e = unet_launch_mx(UCONV_SAME5, planes, k1, st, why);
+        return e != hipSuccess ? e : unet_launch_mx(UCONV_SAME5, planes, k2, st, why);
+    };
+    const char *fe = getenv("MPCD_UNET_FUSE");  // 0: never fuse, 1: fuse whenever a tiling fits, unset: measured
+    const int mode = fe && fe[0] ? atoi(fe) : -1;
+    if (mode == 0) return unfused();
+    hipError_t e = prep_geom(UCONV_SAME5, k1, why);
+    if (e == hipSuccess) e = prep_geom(UCONV_SAME5, k2, why);
+    if (e != hipSuccess) return e;
+    const bool fusable = k1.epi != UEPI_BIAS && k2.epi != UEPI_BIAS && k1.lout == k2.lin && k2.ca == k1.cout &&
+                         k2.cb == 0 && k2.cinp == k1.cout && k2.cout == k1.cout && k2.coutp == k1.coutp &&
+                         (k1.cout & 3) == 0 && k2.rows == k1.rows;
+    if (!fusable) return unfused();
+
+    const int win1 = k1.lin + k1.halo_l + k1.halo_r, win2 = k2.lin + k2.halo_l + k2.halo_r;
+    const int NT = k1.coutp / 16, nprod = planes == 1 ? 1 : 6;
+    const Tile *tiles = planes == 1 ? kTiles1 : kTiles3;
+    const int ntiles = planes == 1 ? 5 : 3;
+    std::vector<RtbChoice> cands;
+    for (int rb = 32; rb >= 1; rb /= 2) {
+        if (rb > 1 && (int64_t)rb > k1.rows) continue;
+        const int ctp = (rb * k1.lout + 15) / 16;
+        const size_t in1 = (size_t)planes * rb * win1 * k1.cs, in2 = (size_t)planes * rb * win2 * k2.cs;
+        const size_t out_b = (size_t)ctp * 16 * (k1.coutp + 4) * 4;
+        const size_t stat_b = (size_t)(2 * rb * 32 + 4) * 4 + (size_t)4 * k1.coutp * 4;
+        const size_t x_off = in1 + out_b;  // >= out_b: the second tile fits in front of x_off
+        const size_t lds = x_off + in2 + stat_b;
+        if (lds > (size_t)160 * 1024) continue;
+        RtbChoice best{};
+        for (int ti = 0; ti < ntiles; ++ti) {
+            const Tile t = tiles[ti];
+            const int jobs = ((NT + t.nn - 1) / t.nn) * ((ctp + t.nc - 1) / t.nc);
+            const int per_wave = (jobs + 3) / 4;
+            const double cyc = (double)per_wave * (k1.kc + k2.kc) *
+                                   (t.nn * t.nc * nprod * 16.0 + t.nn * planes * 24.0 + t.nc * planes * 8.0) +
+                               (double)in1 / 64.0 + 1200.0;
+            const double cost = cyc / rb;
+            if (!best.rb || cost < best.model * 0.999)
+                best = RtbChoice{1, rb, t, lds, (int)x_off, (int)(x_off + in2), cost};
+        }
+        if (best.rb) cands.push_back(best);
+    }
+    if (cands.empty()) return unfused();
+    std::sort(cands.begin(), cands.end(), [](const RtbChoice &x, const RtbChoice &y) { return x.model < y.model; });
+
+    auto key_of = [&](const ConvMK &k) {
+        return MxKey{UCONV_SAME5, planes, k.ca, k.cb, k.cout, k.lin, k.lout, k.epi, k.rows, k.x_rows};
+    };
+    const RtbKey key{key_of(k1), key_of(k2)};
+    RtbChoice pick = cands[0];
+    bool have = false;
+    {
+        std::lock_guard<std::mutex> g(g_mx_mu);
+        auto it = g_rtb_cache.find(key);
+        if (it != g_rtb_cache.end()) {
+            pick = it->second;
+            have = true;
+        }
+    }
+    const bool in_place = k2.out == k1.xa || (k1.xb && k2.out == k1.xb) || (k2.res && k2.out == k2.res) ||
+                          k1.out == k1.xa || (k1.xb && k1.out == k1.xb) || (k2.res && k1.out == k2.res);
+    hipStreamCaptureStatus cap_st = hipStreamCaptureStatusNone;
+    if (!have && mode < 0 && autotune_on() && !in_place && hipStreamIsCapturing(st, &cap_st) == hipSuccess &&
+        cap_st == hipStreamCaptureStatusNone) {
+        // measured against the unfused pair (each conv already on its own measured pick)
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
+            float best_ms = 1e30f;
+            auto timed = [&](const std::function<hipError_t()> &run) -> float {
+                if (run() != hipSuccess) return 1e30f;  // warm-up (and first-use tuning of the unfused convs)
+                (void)hipEventRecord(e0, st);
+                for (int r = 0; r < 2; ++r) (void)run();
+                (void)hipEventRecord(e1, st);
+                float ms = 0.f;
+                if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) return 1e30f;
+                return ms;
+            };
+            const float ms_unf = timed(unfused);
+            if (ms_unf < best_ms) {
+                best_ms = ms_unf;
+                pick = RtbChoice{};
+            }
+            for (const RtbChoice &ch : cands) {
+                const float ms = timed([&] { return launch_rtb_choice(planes, k1, k2, ch, st); });
+                if (ms < best_ms) {
+                    best_ms = ms;
+                    pick = ch;
+                }
+            }
+        }
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        (void)hipGetLastError();
+        std::lock_guard<std::mutex> g(g_mx_mu);
+        g_rtb_cache[key] = pick;
+    }
+    if (mode == 1 && !pick.fused) pick = cands[0];
+    if (!pick.fused) return unfused();
+    return launch_rtb_choice(planes, k1, k2, pick, st);
 }

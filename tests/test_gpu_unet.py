@@ -182,3 +182,28 @@ def test_kat3_through_trained_model_loader(tmp_path):
                          n_diffusion_steps_without_noise=5)
     np.testing.assert_allclose(chain[-1, 0, :8, 0].cpu().numpy(),
                                [0.9998, 0.9592, 0.9130, 0.8686, 0.8263, 0.7862, 0.7497, 0.7155], atol=5e-5)
+
+
+@pytest.mark.parametrize("dtype", ["f32x3", "f16"])
+@pytest.mark.parametrize("d,H,C,B", [(1, 32, 5, 37), (4, 64, 12, 9), (2, 16, 4, 300)])
+def test_fused_block_bit_identical(d, H, C, B, dtype, monkeypatch):
+    """The fused ResidualTemporalBlock launch (conv1's epilogue writes conv2's staged planes in LDS)
+    gives the same bits as the two separate launches, and matches the oracle forward."""
+    net = make_unet(d, C, seed=3 + d)
+    plan = _planner(net, d, H, C, N=50, dtype=dtype)
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(B, H, d, generator=g)
+    ctx = torch.rand(B, C, generator=g) * 2 - 1
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MPCD_UNET_FUSE", mode)
+        out[mode] = plan.eps(x, 31, ctx)
+    for a, b in zip(out["0"], out["1"]):
+        assert torch.equal(a, b)
+    tt = torch.full((B,), 31, dtype=torch.long)
+    with torch.no_grad():
+        rc = net(x, tt, ctx, torch.zeros(B, 1))
+    _close_eps(out["1"][0], rc, f"{dtype} fused d={d} H={H}", EPS_TOL[dtype])
+    full = plan.sample_trajectories(ctx[:1], 40, H, seed=5)
+    monkeypatch.setenv("MPCD_UNET_FUSE", "0")
+    assert torch.equal(full, plan.sample_trajectories(ctx[:1], 40, H, seed=5))
