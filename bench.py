@@ -102,8 +102,8 @@ def cpu_baseline(cfg, budget_s=12.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=None, help="timed control steps (default 20; U-Net configs 3)")
-    ap.add_argument("--warmup", type=int, default=None, help="untimed control steps (default 3; U-Net configs 1)")
+    ap.add_argument("--steps", type=int, default=None, help="timed control steps (default 50; U-Net configs 3)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed control steps (default 20: the shader clock settles over the first dozen launches; U-Net configs 1)")
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -113,8 +113,8 @@ def main():
     cfg = dict(WORKLOADS[args.workload])
     dtype = args.dtype or cfg["dtype"]
     unet = cfg["net"] == "unet"
-    steps = args.steps if args.steps is not None else (3 if unet else 20)
-    warmup = args.warmup if args.warmup is not None else (1 if unet else 3)
+    steps = args.steps if args.steps is not None else (3 if unet else 50)
+    warmup = args.warmup if args.warmup is not None else (1 if unet else 20)
     rank, world, local = _rank_env()
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -57,6 +57,8 @@ struct ConvMK {
     // conv's staged planes (LDS offset nx_off, per-position stride nx_cs, window nx_win, left halo
     // nx_halo_l) instead of storing it to HBM
     int lds_out, nx_off, nx_cs, nx_win, nx_halo_l;
+    // fp16 activation buffers (f16 net): input (xa / xb), residual, output hold halves, not floats
+    int in_h, res_h, out_h;
 };
 
 struct UnetWeights {

@@ -558,6 +558,19 @@ struct Ctx {
     int64_t cp_stride;
     hipStream_t st;
     int li;  // next layer index
+    // f16 net: activation buffers hold fp16 (halves the activation traffic); the sampler state x
+    // (first conv's input) and eps (last conv's output) stay fp32
+    bool act_h;
+    const float *x_in, *eps_out;
+    int act_mask;             // experiment knob (MPCD_UNET_F16_ACT): which buffers are fp16
+    const float *hbuf[8];
+    bool is_h(const float *p) const
+    {
+        if (!act_h || !p) return false;
+        for (int i = 0; i < 8; ++i)
+            if (p == hbuf[i]) return (act_mask >> i) & 1;
+        return false;
+    }
 };
 
 int rows_per_wg(int kind, int lin, int lout, int cinp, int coutp, int halo, size_t &lds)
@@ -630,6 +643,9 @@ ConvMK make_mk(const Ctx &c, const ConvLayer &L, int epi, const float *xa, int c
     k.cout = L.cout;
     k.coutp = L.coutp;
     k.epi = epi;
+    k.in_h = c.is_h(xa);
+    k.res_h = c.is_h(res);
+    k.out_h = c.is_h(out);
     return k;
 }
 
@@ -742,6 +758,10 @@ int forward(Ctx &c, const Dims &m, Buffers &B, const float *x, int64_t x_rows)
 {
     int rc;
     c.li = 0;
+    c.x_in = x;
+    c.eps_out = B.eps;
+    for (int i = 0; i < 5; ++i) c.hbuf[i] = B.buf[i];
+    for (int i = 0; i < 3; ++i) c.hbuf[5 + i] = i + 1 < (int)B.skip.size() ? B.skip[i + 1] : nullptr;
     float *A = B.buf[0], *Bb = B.buf[1], *T = B.buf[2], *R = B.buf[3], *D = B.buf[4];
     const float *cur = x;
     int cc = m.d, L = m.H;
@@ -806,6 +826,11 @@ int unet_sample(const mpcd_net_desc &d, const UnetWeights &W, const UnetSampleAr
     c.cp = a.cproj;
     c.cp_stride = a.cproj_stride;
     c.st = st;
+    {
+        const char *e = getenv("MPCD_UNET_F16_ACT");  // experiment knob: 0 keeps fp32 activations
+        c.act_mask = e && e[0] ? atoi(e) : 255;
+        c.act_h = W.planes == 1 && c.act_mask != 0;
+    }
     const int threads = 256;
     const int64_t nq = a.batch * (flat / 4);
     const unsigned g1 = (unsigned)((nq + threads - 1) / threads);

@@ -41,6 +41,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -225,7 +226,10 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
         return xr;
     };
     // one 16-byte item (8 channels of one position of one row): source pointer (or null = zeros), LDS dest
-    auto item = [&](int64_t r0, int nrow, int i, const float *&src, int &dst) {
+    // activations in HBM: fp32, or (in_h, f16 net only) fp16 - 8 channels = one 16-byte load that is
+    // already the staged f16 plane
+    const int esh = a.in_h ? 1 : 2;
+    auto item = [&](int64_t r0, int nrow, int i, const char *&src, int &dst) {
         int g8, pw;
         const int rp = qdiv(i, g8n, inv_g8n, g8);
         const int r = qdiv(rp, win, inv_win, pw);
@@ -234,11 +238,21 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
         src = nullptr;
         if (r < nrow && p >= 0 && p < a.lin && ci < cin) {
             const int64_t xr = xrow(r0, r);
-            src = ci < a.ca ? a.xa + ((size_t)xr * a.lin + p) * a.ca + ci
-                            : a.xb + ((size_t)xr * a.lin + p) * a.cb + (ci - a.ca);
+            src = ci < a.ca ? reinterpret_cast<const char *>(a.xa) + ((((size_t)xr * a.lin + p) * a.ca + ci) << esh)
+                            : reinterpret_cast<const char *>(a.xb) + ((((size_t)xr * a.lin + p) * a.cb + (ci - a.ca)) << esh);
         }
     };
+    auto fetch = [&](const char *src, f32x4 &lo, f32x4 &hi) {  // in_h: the 8 halves' bits in lo
+        const float *s = src ? reinterpret_cast<const float *>(src) : a.xa;
+        lo = ldg4(s);
+        hi = a.in_h ? f32x4{0.f, 0.f, 0.f, 0.f} : ldg4(s + 4);
+        if (!src) lo = hi = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
     auto put = [&](int dst, const f32x4 &lo, const f32x4 &hi) {
+        if (P == 1 && a.in_h) {
+            *reinterpret_cast<f32x4 *>(sm + a.in_off + dst) = lo;
+            return;
+        }
         u32x4 o[P];
         split8<P>(lo, hi, o);
 #pragma unroll
@@ -252,11 +266,9 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
                 int dst[SU];
 #pragma unroll
                 for (int u = 0; u < SU; ++u) {
-                    const float *src;
+                    const char *src;
                     item(r0, nrow, min(i0 + u * MT, n_items - 1), src, dst[u]);
-                    lo[u] = ldg4(src ? src : a.xa);
-                    hi[u] = ldg4(src ? src + 4 : a.xa);
-                    if (!src) lo[u] = hi[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    fetch(src, lo[u], hi[u]);
                 }
 #pragma unroll
                 for (int u = 0; u < SU; ++u)
@@ -291,12 +303,10 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
 #pragma unroll
         for (int u = 0; u < (PERS ? SUP : 1); ++u) {
             const int i = tid + u * MT;
-            const float *src;
+            const char *src;
             item(r0, nrow, min(i, n_items - 1), src, pre_dst[u]);
             if (i >= n_items) pre_dst[u] = -1;
-            pre_lo[u] = ldg4(src ? src : a.xa);
-            pre_hi[u] = ldg4(src ? src + 4 : a.xa);
-            if (!src) pre_lo[u] = pre_hi[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+            fetch(src, pre_lo[u], pre_hi[u]);
         }
     };
     auto stage_commit = [&]() {
@@ -511,8 +521,17 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
             for (int u = 0; u < EU; ++u) {
                 const int ro = min(i0 + u * tps, n_ro - 1);  // clamped: a duplicate item is recomputed, not stored
                 rr[u] = qdiv(ro, a.lout, inv_lout, oo_[u]);
-                if (epi == UEPI_GN_MISH_RES)
-                    rv[u] = ldg4(a.res + ((size_t)(r0 + rr[u]) * a.lout + oo_[u]) * a.cout + co_t);
+                if (epi == UEPI_GN_MISH_RES) {
+                    const size_t e = ((size_t)(r0 + rr[u]) * a.lout + oo_[u]) * a.cout + co_t;
+                    if (a.res_h) {
+                        // one f16x4 load + convertvector (bit-casting the two dwords of a u32x2 load
+                        // separately compiled to a single-dword load whose halves were reused)
+                        const f16x4 h = *reinterpret_cast<const f16x4 *>(reinterpret_cast<const char *>(a.res) + 2 * e);
+                        rv[u] = __builtin_convertvector(h, f32x4);
+                    } else {
+                        rv[u] = ldg4(a.res + e);
+                    }
+                }
             }
 #pragma unroll
             for (int u = 0; u < EU; ++u) {
@@ -546,6 +565,11 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
                     char *d = sm + a.nx_off + r * nrowB + (oo + a.nx_halo_l) * a.nx_cs + co_t * 2;
 #pragma unroll
                     for (int pl = 0; pl < P; ++pl) *reinterpret_cast<u32x2 *>(d + pl * a.rb * nrowB) = o[pl];
+                    continue;
+                }
+                if (a.out_h) {  // fp16 activation (cout % 4 == 0, host-checked)
+                    *reinterpret_cast<u32x2 *>(reinterpret_cast<char *>(a.out) + 2 * (((size_t)grow * a.lout + oo) * a.cout + co_t)) =
+                        u32x2{pk_f16(v.x, v.y), pk_f16(v.z, v.w)};
                     continue;
                 }
                 float *dst = a.out + ((size_t)grow * a.lout + oo) * a.cout + co_t;
@@ -771,6 +795,11 @@ hipError_t prep_geom(int kind, ConvMK &k, std::string *why)
     int cs = cinp * 2;
     if (((cs / 16) & 1) == 0) cs += 16;
     k.cs = cs;
+    if ((k.in_h || k.res_h || k.out_h) &&
+        (cinp != k.cinp || (k.in_h && ((k.ca & 7) || (k.cb & 7))) || (k.out_h && (k.cout & 3)))) {
+        if (why) *why = "UNet mx conv: fp16 activations need 8-channel input groups and 4-channel output groups";
+        return hipErrorInvalidValue;
+    }
     if (k.epi != UEPI_BIAS) {
         const int cpg = k.cout / k.groups;
         int sh = 0;
