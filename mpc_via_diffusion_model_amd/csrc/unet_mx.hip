@@ -21,6 +21,7 @@
 // through LDS (reusing the staged input when one job per wave suffices) for the GroupNorm statistics
 // (fp64, shifted) and the elementwise epilogue, stored coalesced channels-last.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -752,6 +753,15 @@ bool autotune_on()
     return on;
 }
 
+bool tune_log()  // MPCD_UNET_TUNE_LOG=1: print every measured candidate (stderr)
+{
+    static const bool on = [] {
+        const char *e = getenv("MPCD_UNET_TUNE_LOG");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 hipError_t launch_choice(int kind, int planes, ConvMK &k, const MxChoice &ch, hipStream_t st)
 {
     k.rb = ch.rb;
@@ -944,6 +954,10 @@ hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::
                 (void)hipEventRecord(e1, st);
                 float ms = 0.f;
                 if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) continue;
+                if (tune_log())
+                    fprintf(stderr, "[mx tune] kind %d P%d cin %d+%d cout %d L %d->%d epi %d rows %lld: rb %d tile %dx%d %s %.1f us\n",
+                            kind, planes, k.ca, k.cb, k.cout, k.lin, k.lout, k.epi, (long long)k.rows, ch.rb, ch.t.nn,
+                            ch.t.nc, ch.pers ? "pers" : ch.alias ? "alias" : "tile", ms * 500.f);
                 if (ms < best_ms) {
                     best_ms = ms;
                     pick = ch;
@@ -1111,8 +1125,13 @@ hipError_t unet_launch_mx_rtb(int planes, ConvMK &k1, ConvMK &k2, hipStream_t st
                 best_ms = ms_unf;
                 pick = RtbChoice{};
             }
+            if (tune_log())
+                fprintf(stderr, "[rtb tune] P%d cin %d+%d cout %d L %d rows %lld: unfused %.1f us\n", planes, k1.ca, k1.cb,
+                        k1.cout, k1.lin, (long long)k1.rows, ms_unf * 500.f);
             for (const RtbChoice &ch : cands) {
                 const float ms = timed([&] { return launch_rtb_choice(planes, k1, k2, ch, st); });
+                if (tune_log())
+                    fprintf(stderr, "[rtb tune]   fused rb %d tile %dx%d %.1f us\n", ch.rb, ch.t.nn, ch.t.nc, ms * 500.f);
                 if (ms < best_ms) {
                     best_ms = ms;
                     pick = ch;
