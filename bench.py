@@ -59,22 +59,73 @@ def _rank_env():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
 
 
+def synthetic_params(spec, seed=0):
+    """Random-init weights of the net's architecture without the oracle: PyTorch's default init restated
+    per tensor of the library's parameter list (mpcd_net_param_info): Linear / Conv1d / ConvTranspose1d
+    weights and biases ~ U(-1/sqrt(fan_in), 1/sqrt(fan_in)) (kaiming_uniform_(a=sqrt(5)); fan_in =
+    size(1) * kernel size, as torch computes it), GroupNorm weight 1 and bias 0. Seeded, CPU."""
+    from mpc_via_diffusion_model_amd import _native as N
+    g = torch.Generator().manual_seed(seed)
+    specs = N.param_spec(spec.desc())
+    shapes = dict(specs)
+    out = {}
+    for name, shp in specs:
+        if len(shp) >= 2:
+            fan_in = shp[1] * int(np.prod(shp[2:], dtype=np.int64))
+        else:
+            wshape = shapes.get(name[:-len("bias")] + "weight") if name.endswith("bias") else None
+            if wshape is None or len(wshape) < 2:  # GroupNorm affine
+                out[name] = torch.ones(shp) if name.endswith("weight") else torch.zeros(shp)
+                continue
+            fan_in = wshape[1] * int(np.prod(wshape[2:], dtype=np.int64))
+        b = 1.0 / np.sqrt(fan_in)
+        out[name] = (torch.rand(shp, generator=g, dtype=torch.float64) * 2 - 1).mul(b).float()
+    return out
+
+
 def _net(cfg):
-    from oracle import nets  # random-init weights of the net's architecture (seed 0), test infra only
+    from oracle import nets  # the CPU baseline's torch module (test infrastructure, cpu_baseline leg only)
     torch.manual_seed(0)
     if cfg["net"] == "mlp":
         return nets.ConditionedMLPNet(state_dim=cfg["d"], horizon=cfg["H"], context_dim=cfg["C"]).eval()
     return nets.ConditionedTemporalUnet(state_dim=cfg["d"], context_dim=cfg["C"]).eval()
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_share():
+    """CPUs this process may actually use: os.cpu_count() shows the whole machine on a shared GPU box,
+    the affinity mask and the cgroup CPU quota show its share."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def cpu_baseline(cfg, budget_s=12.0):
-    """The oracle (torch-CPU restatement of the reference path, 'port') on this host's cores:
-    normalise -> CFG sampler (2 forwards/step) -> unnormalise -> fp64 C rollout/cost -> argmin."""
+    """The oracle (torch-CPU restatement of the reference path, 'port') on this host's cores, SURVEY §8d:
+    every CPU this process may use (torch.set_num_threads), B_cpu = min(B, 256) candidates per control
+    step, full N: normalise -> CFG sampler (2 forwards/step) -> unnormalise -> fp64 C rollout/cost -> argmin.
+    At least one control step, then as many as fit the budget."""
     from oracle import normalizer, sampler, schedule
     from oracle import systems as osys
-    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+    threads = _cpu_share()
     torch.set_num_threads(threads)
-    b_cpu = min(cfg["B"], 256 if cfg["net"] == "mlp" else 16)
+    b_cpu = min(cfg["B"], 256)
     net = _net(cfg)
     bufs = schedule.buffers(cfg["schedule"], cfg["N"])
     rng = np.random.default_rng(1)
@@ -95,15 +146,19 @@ def cpu_baseline(cfg, budget_s=12.0):
         if el >= budget_s:
             break
     return {"value": done / el, "unit": "candidate trajectories/s", "cores": threads, "kind": "port",
-            "sample": f"{done // b_cpu} mpc_steps x {b_cpu} candidates (N={cfg['N']}, H={cfg['H']}) in {el:.1f} s; "
-                      "per-candidate cost is linear in B"}
+            "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
+            "sample": f"{done // b_cpu} mpc_steps x {b_cpu} candidates (N={cfg['N']}, H={cfg['H']}) in {el:.1f} s "
+                      f"on {threads} threads ({_cpu_model()}; {os.cpu_count()} CPUs on the host, {threads} in this "
+                      f"process's share); per-candidate cost is linear in B, so cand/s at B={cfg['B']} is the same"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=None, help="timed control steps (default 50; U-Net configs 3)")
-    ap.add_argument("--warmup", type=int, default=None, help="untimed control steps (default 20: the shader clock settles over the first dozen launches; U-Net configs 1)")
+    ap.add_argument("--steps", type=int, default=None, help="timed control steps (default 50; U-Net configs 5)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed control steps (default 20: the shader clock settles over the first dozen launches; U-Net configs 2, the first one runs the tiling autotune)")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong (SURVEY §8d: fixed B_total split over the ranks) or weak (B per rank)")
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -113,8 +168,8 @@ def main():
     cfg = dict(WORKLOADS[args.workload])
     dtype = args.dtype or cfg["dtype"]
     unet = cfg["net"] == "unet"
-    steps = args.steps if args.steps is not None else (3 if unet else 50)
-    warmup = args.warmup if args.warmup is not None else (1 if unet else 20)
+    steps = args.steps if args.steps is not None else (5 if unet else 50)
+    warmup = args.warmup if args.warmup is not None else (2 if unet else 20)
     rank, world, local = _rank_env()
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -122,7 +177,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
-    if cfg["split"]:
+    if args.scaling == "strong":
         if cfg["B"] % world:
             raise SystemExit(f"{args.workload}: {cfg['B']} candidates do not split over {world} ranks")
         b_local, scaling = cfg["B"] // world, "strong"
@@ -132,10 +187,9 @@ def main():
     from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec, systems
     from mpc_via_diffusion_model_amd import distributed as D
 
-    net = _net(cfg)
     spec = NetSpec(cfg["net"], state_dim=cfg["d"], horizon=cfg["H"], context_dim=cfg["C"], dtype=dtype)
-    plan = DiffusionMPC(spec, net.state_dict(), variance_schedule=cfg["schedule"], n_diffusion_steps=cfg["N"])
-    del net
+    plan = DiffusionMPC(spec, synthetic_params(spec, seed=0), variance_schedule=cfg["schedule"],
+                        n_diffusion_steps=cfg["N"])
     system = systems.get(cfg["system"])
     assert system.n_x == cfg["C"] and system.n_u == cfg["d"]
     rng = np.random.default_rng(1)
@@ -168,6 +222,24 @@ def main():
         elapsed, kms = float(t[0]), float(t[1])
     else:
         kms = float(np.mean(kernel_ms))
+
+    # strong scaling: what each of 8 GPUs would run (B_total / 8 candidates), measured here on one GPU
+    shard_probe = None
+    if world == 1 and scaling == "strong" and not unet and cfg["B"] % 8 == 0:
+        b8 = cfg["B"] // 8
+        for i in range(5):
+            plan.mpc_step(x0s[i % len(x0s)], system, b8, w=0.01, sample_fn=cfg["sampler"], ddim_steps=cfg["ddim_steps"],
+                          seed=100 + i)
+        torch.cuda.synchronize()
+        t1, n1 = time.perf_counter(), max(steps, 20)
+        for i in range(n1):
+            plan.mpc_step(x0s[i % len(x0s)], system, b8, w=0.01, sample_fn=cfg["sampler"], ddim_steps=cfg["ddim_steps"],
+                          seed=200 + i)
+        torch.cuda.synchronize()
+        el1 = time.perf_counter() - t1
+        shard_probe = {"candidates": b8, "value": b8 * n1 / el1, "ms_per_step": 1e3 * el1 / n1,
+                       "note": f"one GPU running the B_total/8 = {b8}-candidate shard each of 8 GPUs gets under strong "
+                               "scaling (before the exchange); x8 is the compute-only 8-GPU bound"}
 
     if rank == 0:
         total = b_local * world * steps
@@ -219,7 +291,8 @@ def main():
             "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f16" if dtype == "f16" else "f32",
-            "data": f"synthetic (random-init weights seed 0, x0 ~ U[-1,1]^{cfg['C']}, Philox noise)",
+            "data": f"synthetic (random-init weights seed 0 by PyTorch's default-init rule, x0 ~ U[-1,1]^{cfg['C']}, "
+                    "Philox noise)",
             "config": {"workload": cfg["workload"], "candidates_per_gpu": b_local, "candidates_total": b_local * world,
                        "horizon": cfg["H"], "action_dim": cfg["d"], "context_dim": cfg["C"], "denoise_steps": n_evals,
                        "sampler": f"{'CFG-DDIM' if cfg['sampler'] == 'ddim_cfg' else 'CFG-DDPM'} w=0.01",
@@ -228,6 +301,8 @@ def main():
             "roofline": dict(roof, traffic=traffic, kernel_ms=kms, timed=timed),
             "best_cost_last_step": r.best_cost,
         }
+        if shard_probe:
+            out["strong_shard_probe"] = shard_probe
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_budget)
         else:

@@ -13,6 +13,10 @@
  *    during the call only. Weights, schedule, plan and workspace belong to the context.
  *  - Work is enqueued on the caller's HIP stream (void* hip_stream; NULL = legacy default stream)
  *    and is asynchronous unless stated otherwise. One context per device; not thread-safe.
+ *  - A context owns workspace (plan, projections, U-Net activations, reduction counters) that
+ *    consecutive calls reuse: issue a context's calls on ONE stream, or order the streams yourself
+ *    (hipStreamWaitEvent) before switching. The cached step plan / time projections are the exception:
+ *    a call on another stream waits for them by itself.
  *  - All trajectory tensors are fp32 row-major [B][H][d] (candidate, horizon, action dim), the
  *    layout of the reference's x in cart_pole_sample_loop (diffusion_model_base.py:188-189).
  */
@@ -35,6 +39,8 @@ enum mpcd_status {
     MPCD_ESTATE = -3,   /* missing net / schedule, or call out of order */
     MPCD_ENOMEM = -4,
     MPCD_EUNSUP = -5,   /* configuration the kernels do not implement */
+    MPCD_ENONFINITE = -6, /* mpcd_mpc_step: no candidate has a finite cost (NaN / Inf samples or rollout) -
+                             the result block is still written; see mpcd_last_step_flags */
 };
 
 enum mpcd_net_kind {
@@ -113,7 +119,17 @@ typedef struct {
                                   slice 0 = x_T, slice k = the draw of denoise step k */
     float *x_out;              /* dev [B][H][d] final normalised sample */
     float *chain_out;          /* dev [S+1][B][H][d] or NULL (run_CFG return_chain, :403-415) */
+    float *chain_absmax;       /* dev [B] or NULL: per candidate, max |x| over every chain slice x_T .. x_0
+                                  (NaN if any element is NaN) - what LimitsNormalizer's global clip test
+                                  sees when the caller unnormalises the whole chain (see mpcd_clip_rule) */
 } mpcd_sample_args;
+
+/* The sampler's in-kernel noise stream (Philox4x32-10 keyed by seed, global candidate index, slice,
+ * element quad) for candidates [global_offset, global_offset + n_cand): out dev [n_slices][n_cand][flat]
+ * fp32, slice 0 = x_T, slice k = the draw of denoise step k (what `noise` would have to hold to replay
+ * a Philox run in injected-noise mode). flat = H*d, a multiple of 4. */
+int mpcd_philox_noise(uint64_t seed, int64_t global_offset, int64_t n_cand, int32_t n_slices, int32_t flat,
+                      float *out, void *hip_stream);
 
 /* Number of denoise steps S a call makes (DDPM: N + n_wo_noise; DDIM: grid pairs). */
 int mpcd_sample_steps(mpcd_ctx *ctx, const mpcd_sample_args *args, int32_t *n_steps);
@@ -148,8 +164,11 @@ typedef struct {
     double Q[12], R[4], P[12], x_ref[12];   /* diagonal weights and set-point, fp64 */
 } mpcd_system_desc;
 
-/* Global clip flag of LimitsNormalizer.unnormalize (normalization.py:160-162): *flag_dev = 1 iff some
- * x[i] > 1+1e-4 or < -1-1e-4 over the n values, else 0. Sharded callers OR the per-rank flags. */
+/* Global clip flag of LimitsNormalizer.unnormalize (normalization.py:160-162): *flag_dev = 1 iff
+ * x.max() > 1+1e-4 or x.min() < -1-1e-4 over the n values, with torch's NaN semantics (a NaN anywhere
+ * makes max/min NaN and both tests false: flag 0). Also valid over mpcd_sample's chain_absmax values.
+ * Sharded callers max-reduce the per-rank flags (a NaN on any rank is reported as flag value 2, which
+ * a max-reduction keeps: only 1 means clip). */
 int mpcd_clip_flag(mpcd_ctx *ctx, const float *x, int64_t n, int32_t *flag_dev, void *hip_stream);
 
 /* Unnormalise (LimitsNormalizer.unnormalize, normalization.py:156-167; clip iff the GLOBAL max/min of
@@ -180,8 +199,9 @@ int mpcd_argmin(mpcd_ctx *ctx, const double *cost, int64_t n, int64_t index_offs
  * own group of `group` consecutive candidates, no host round trip inside the loop
  * (Cart_Diffusion_inference.py:405-512 runs one state at a time on the host). */
 
-/* Per-group clip flags: flags_dev[g] = 1 iff some x in [g*group_elems, (g+1)*group_elems) leaves
- * [-1-1e-4, 1+1e-4] (LimitsNormalizer's rule applied to each state's own candidate batch). */
+/* Per-group clip flags: flags_dev[g] = mpcd_clip_flag's code over x[g*group_elems, (g+1)*group_elems)
+ * (LimitsNormalizer's rule applied to each state's own candidate batch, or to its candidates'
+ * chain_absmax values: 1 = clip). */
 int mpcd_clip_flags(mpcd_ctx *ctx, const float *x, int64_t n_groups, int64_t group_elems, int32_t *flags_dev,
                     void *hip_stream);
 
@@ -214,6 +234,12 @@ int mpcd_control_step(mpcd_ctx *ctx, const mpcd_system_desc *sys, double *x_dev,
 /* Rank 0 creates the id (ncclGetUniqueId) and ships its 128 bytes to every rank out of band. */
 int mpcd_comm_unique_id(void *id_out);
 int mpcd_comm_init(mpcd_ctx *ctx, int32_t nranks, int32_t rank, const void *id);
+/* Loopback communicator: `nranks` VIRTUAL ranks = nranks contexts on the same device in one process,
+ * each context driven by its own host thread, joined by a caller-chosen group_key. The collectives are
+ * device copies ordered by HIP events plus a host rendezvous of the member threads (120 s timeout), so
+ * mpcd_select / mpcd_mpc_step run their N-rank code (rank offsets, gathered-cost order, owner-row sum,
+ * flag max-reduction) on one GPU: the single-GPU rehearsal and test of the RCCL path. */
+int mpcd_comm_init_loopback(mpcd_ctx *ctx, int32_t nranks, int32_t rank, uint64_t group_key);
 int mpcd_comm_info(mpcd_ctx *ctx, int32_t *nranks, int32_t *rank);  /* 1, 0 without mpcd_comm_init */
 /* recv [nranks * count_per_rank] (rank order); without a communicator: a device copy. */
 int mpcd_allgather_f32(mpcd_ctx *ctx, const float *send, float *recv, size_t count_per_rank, void *hip_stream);
@@ -232,6 +258,13 @@ int mpcd_select(mpcd_ctx *ctx, const double *cost_local, int64_t n_local, const 
  * every candidate -> argmin -> applied action) for this rank's shard, plus the exchange of mpcd_select
  * when the context has a communicator. Everything stays on the device until one D2H copy of the
  * result; the call then synchronises the stream, so best_host / u_best_host are valid on return. */
+/* The reference scripts call run_CFG(..., return_chain=True) and unnormalise the WHOLE chain
+ * (Cart_Diffusion_inference.py:450-463, Diffusion_MPC_Inference.py:232-247), so the clip test sees x_T
+ * ~ N(0, 1) as well and practically always clips. MPCD_CLIP_CHAIN reproduces that (the default);
+ * MPCD_CLIP_FINAL tests the final samples only (a caller that unnormalises just x_0); MPCD_CLIP_NONE: the
+ * caller has proven the final-only flag 0 (DDPM whose last posterior mean cannot leave [-1, 1]). */
+enum mpcd_clip_rule { MPCD_CLIP_CHAIN = 0, MPCD_CLIP_FINAL = 1, MPCD_CLIP_NONE = 2 };
+
 typedef struct {
     const mpcd_system_desc *sys;   /* n_u == the net's state_dim */
     const double *x0;              /* host [n_x] fp64 plant state */
@@ -239,17 +272,39 @@ typedef struct {
                                       (LimitsNormalizer.normalize, normalization.py:149-154) */
     const float *act_min, *act_max; /* host [d] action limits (LimitsNormalizer.unnormalize, :156-167) */
     mpcd_sample_args sample;       /* .context / .context_shared are ignored (the normalised x0 is the shared
-                                      context); .batch = B_local; .global_offset = rank * B_local; .x_out required */
-    int32_t flag_zero;             /* 1: the caller has proven the global clip flag 0 (DDPM whose last posterior
-                                      mean cannot leave [-1, 1]) - no flag reduction is run */
+                                      context); .batch = B_local; .global_offset = rank * B_local; .x_out required;
+                                      .chain_absmax is set by the call itself under MPCD_CLIP_CHAIN */
+    int32_t clip_rule;             /* mpcd_clip_rule: which tensor LimitsNormalizer's global clip test runs over */
     double *cost_local;            /* dev [batch] fp64 costs of this rank's candidates (out) */
     double *costs_all;             /* dev [nranks * batch] all costs (out), needed with a communicator, else unused */
 } mpcd_step_args;
 
 /* best_host: global winner (index over all ranks); u_best_host: host [H*d] fp32, the winner's
- * UNnormalised trajectory (u_best[0] is the applied action before the reference's rounding). */
+ * UNnormalised trajectory (u_best[0] is the applied action before the reference's rounding).
+ * Returns MPCD_ENONFINITE (outputs written) when the winning cost is not finite, i.e. every candidate of
+ * every rank is NaN / Inf - garbage is never returned as a normal result. */
 int mpcd_mpc_step(mpcd_ctx *ctx, const mpcd_step_args *args, mpcd_best *best_host, float *u_best_host,
                   void *hip_stream);
+
+/* Failure-detection flags of the last mpcd_mpc_step on this context (read after it returned):
+ * bit 0 (MPCD_STEP_CLIPPED): LimitsNormalizer's global clip was applied; bit 1 (MPCD_STEP_NAN_SAMPLES): some
+ * candidate's tested tensor (its chain under MPCD_CLIP_CHAIN, its final sample under MPCD_CLIP_FINAL) holds a
+ * NaN on some rank - the reference's torch max()/min() are then NaN and nothing is clipped; bit 2
+ * (MPCD_STEP_NONFINITE_WINNER): no finite cost (the call returned MPCD_ENONFINITE). */
+enum { MPCD_STEP_CLIPPED = 1, MPCD_STEP_NAN_SAMPLES = 2, MPCD_STEP_NONFINITE_WINNER = 4 };
+int mpcd_last_step_flags(mpcd_ctx *ctx, int32_t *flags);
+
+/* U-Net conv tilings (MPCD_F32X3 / MPCD_F16). Each conv launch picks rows-per-workgroup x register tile
+ * x persistent-or-not among candidates by timing them once per layer shape and batch, and each
+ * ResidualTemporalBlock picks fused-or-not the same way. This process-wide override makes the choice
+ * deterministic, so a caller can run EVERY candidate on its own batch (they are bit-identical: the
+ * K order and the GroupNorm summation order do not depend on the tiling):
+ *   conv_pick  -1 = measured (default); i >= 0 = candidate (i mod count) for every conv, blocks unfused
+ *              unless block_pick says otherwise;
+ *   block_pick -1 = measured; -2 = never fuse; i >= 0 = fused candidate (i mod count) for every block. */
+int mpcd_unet_force_tiling(int32_t conv_pick, int32_t block_pick);
+#define MPCD_UNET_MAX_CONV_TILINGS 12   /* 6 rows-per-workgroup values x {tiled, persistent} */
+#define MPCD_UNET_MAX_BLOCK_TILINGS 6
 
 /* Timing of the last mpcd_sample's main kernel (HIP events on the call's stream), milliseconds.
  * Blocks until that kernel has finished. */

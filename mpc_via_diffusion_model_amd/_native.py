@@ -18,8 +18,11 @@ MPCD_F32, MPCD_F16, MPCD_F32X3 = 0, 1, 2
 MPCD_DDPM_CFG, MPCD_DDIM_CFG, MPCD_DDIM = 0, 1, 2
 MPCD_COST_CANONICAL, MPCD_COST_CALMPC = 0, 1
 MPCD_COMM_ID_BYTES = 128
+MPCD_CLIP_CHAIN, MPCD_CLIP_FINAL, MPCD_CLIP_NONE = 0, 1, 2
 
-_STATUS = {-1: "EINVAL", -2: "EHIP", -3: "ESTATE", -4: "ENOMEM", -5: "EUNSUP"}
+_STATUS = {-1: "EINVAL", -2: "EHIP", -3: "ESTATE", -4: "ENOMEM", -5: "EUNSUP", -6: "ENONFINITE"}
+MPCD_ENONFINITE = -6
+MPCD_STEP_CLIPPED, MPCD_STEP_NAN_SAMPLES, MPCD_STEP_NONFINITE_WINNER = 1, 2, 4
 
 
 class NetDesc(ctypes.Structure):
@@ -35,7 +38,7 @@ class SampleArgs(ctypes.Structure):
                 ("ddim_steps", ctypes.c_int32), ("clamp_x0", ctypes.c_int32), ("n_ddim_times", ctypes.c_int32),
                 ("ddim_times", ctypes.POINTER(ctypes.c_int32)), ("seed", ctypes.c_uint64),
                 ("global_offset", ctypes.c_int64), ("noise", ctypes.c_void_p), ("x_out", ctypes.c_void_p),
-                ("chain_out", ctypes.c_void_p)]
+                ("chain_out", ctypes.c_void_p), ("chain_absmax", ctypes.c_void_p)]
 
 
 class SystemDesc(ctypes.Structure):
@@ -51,7 +54,7 @@ class Best(ctypes.Structure):
 class StepArgs(ctypes.Structure):
     _fields_ = [("sys", ctypes.POINTER(SystemDesc)), ("x0", ctypes.c_void_p), ("ctx_min", ctypes.c_void_p),
                 ("ctx_max", ctypes.c_void_p), ("act_min", ctypes.c_void_p), ("act_max", ctypes.c_void_p),
-                ("sample", SampleArgs), ("flag_zero", ctypes.c_int32), ("cost_local", ctypes.c_void_p),
+                ("sample", SampleArgs), ("clip_rule", ctypes.c_int32), ("cost_local", ctypes.c_void_p),
                 ("costs_all", ctypes.c_void_p)]
 
 
@@ -92,6 +95,11 @@ EXPORTS = {
                            ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "mpcd_comm_unique_id": ([ctypes.c_void_p], ctypes.c_int),
     "mpcd_comm_init": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p], ctypes.c_int),
+    "mpcd_philox_noise": ([ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                           ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "mpcd_last_step_flags": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+    "mpcd_unet_force_tiling": ([ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
+    "mpcd_comm_init_loopback": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64], ctypes.c_int),
     "mpcd_comm_info": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "mpcd_allgather_f32": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p],
                            ctypes.c_int),
@@ -110,7 +118,9 @@ _lib = None
 
 
 class MpcdError(RuntimeError):
-    pass
+    def __init__(self, msg, status=None):
+        super().__init__(msg)
+        self.status = status
 
 
 def lib():
@@ -132,7 +142,7 @@ def lib():
 def check(rc, what):
     if rc != 0:
         msg = lib().mpcd_last_error().decode(errors="replace")
-        raise MpcdError(f"{what} failed ({_STATUS.get(rc, rc)}): {msg}")
+        raise MpcdError(f"{what} failed ({_STATUS.get(rc, rc)}): {msg}", rc)
 
 
 def param_spec(desc):

@@ -16,7 +16,7 @@ CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(PKG, "libmpcd.so")
 OBJ = os.path.join(PKG, "_build")
 ARCH = os.environ.get("MPCD_OFFLOAD_ARCH", "gfx950")
-SOURCES = ["mpcd_api.hip", "mlp_sampler.hip", "mlp_x3.hip", "cond_prologue.hip", "rollout.hip", "unet.hip", "unet_mx.hip"]
+SOURCES = ["mpcd_api.hip", "comm.hip", "mlp_sampler.hip", "mlp_x3.hip", "cond_prologue.hip", "rollout.hip", "unet.hip", "unet_mx.hip"]
 # -amdgpu-mfma-vgpr-form: MFMA accumulators in VGPRs (no v_accvgpr_read before every epilogue op;
 # f32 MFMA and VALU share issue on gfx950, so those moves cost MFMA time).
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}", "-mllvm", "-amdgpu-mfma-vgpr-form", "-Wall",
@@ -50,6 +50,15 @@ def build(force=False, verbose=False, variant=None, defines=()):
         out = os.path.join(PKG, f"libmpcd_{variant}.so")
         obj = OBJ + "_" + variant
         flags += [f"-D{d}" for d in defines]
+        # experiment builds only: MPCD_DROP_FLAGS / MPCD_EXTRA_FLAGS (space separated) edit the compile line
+        drop = os.environ.get("MPCD_DROP_FLAGS", "").split()
+        for f in drop:
+            while f in flags:
+                i = flags.index(f)
+                del flags[i]
+                if i > 0 and flags[i - 1] == "-mllvm":
+                    del flags[i - 1]
+        flags += os.environ.get("MPCD_EXTRA_FLAGS", "").split()
     os.makedirs(obj, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     headers.append(os.path.join(os.path.dirname(PKG), "include", "mpcd.h"))

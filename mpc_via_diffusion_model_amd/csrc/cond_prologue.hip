@@ -92,3 +92,28 @@ void launch_ctx_prologue(const float *ctx, int64_t n_rows, int ctx_dim, const Co
     hipLaunchKernelGGL(ctx_prologue_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, ctx, n_rows,
                        ctx_dim, layers_dev, n_layers, cond_dim, cond_total, cproj);
 }
+
+// The samplers' in-kernel noise for candidates [goff, goff + n): out[k][b][4q..4q+3] =
+// philox_normal4(seed, goff + b, k, q) - the same call the MLP / U-Net kernels make for slice k.
+__global__ void philox_noise_kernel(uint64_t seed, int64_t goff, int64_t n, int n_slices, int quads, float *out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per = n * quads;
+    if (i >= per * n_slices) return;
+    const int k = (int)(i / per);
+    const int64_t r = i - (int64_t)k * per;
+    const int64_t b = r / quads;
+    const int q = (int)(r - b * quads);
+    *reinterpret_cast<f32x4 *>(out + 4 * i) = philox_normal4(seed, (uint64_t)(goff + b), (uint32_t)k, (uint32_t)q);
+}
+
+hipError_t launch_philox_noise(uint64_t seed, int64_t goff, int64_t n, int n_slices, int flat, float *out,
+                               hipStream_t stream)
+{
+    const int64_t total = n * (flat / 4) * n_slices;
+    const int64_t blocks = (total + 255) / 256;
+    if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(philox_noise_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, seed, goff, n, n_slices,
+                       flat / 4, out);
+    return hipGetLastError();
+}

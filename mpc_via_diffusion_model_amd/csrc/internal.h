@@ -24,6 +24,10 @@ void launch_time_prologue(const StepPlan *plan, int n_steps, const float *time_w
 void launch_ctx_prologue(const float *ctx, int64_t n_rows, int ctx_dim, const CondLayer *layers_dev, int n_layers,
                          int cond_dim, int cond_total, float *cproj, hipStream_t stream);
 
+// The samplers' Philox noise stream for candidates [goff, goff + n): out [n_slices][n][flat] (mpcd_philox_noise)
+hipError_t launch_philox_noise(uint64_t seed, int64_t goff, int64_t n, int n_slices, int flat, float *out,
+                               hipStream_t stream);
+
 struct MlpSampleArgs {
     const float *wpack;      // packed linear layers (see mlp_sampler.hip)
     const StepPlan *plan;    // [S]
@@ -33,6 +37,7 @@ struct MlpSampleArgs {
     const float *noise;      // [S+1][B][D0] or null
     float *x_out;            // [B][D0]
     float *chain;            // [S+1][B][D0] or null
+    float *chain_absmax;     // [B] or null: max |x| over the chain per candidate (bits of a NaN if any)
     int64_t batch;
     int64_t global_offset;
     uint64_t seed;

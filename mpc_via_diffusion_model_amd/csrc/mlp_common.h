@@ -64,4 +64,23 @@ MPCD_DEV StepPlan load_plan(const StepPlan *plan, int s)
     return r;
 }
 
+// |v| as an ordered integer: max over these bits is max |v| and propagates a NaN (its magnitude bits
+// exceed +inf's), which is what the chain clip test needs (mpcd_sample_args.chain_absmax).
+MPCD_DEV uint32_t abs_bits(float v) { return __builtin_bit_cast(uint32_t, v) & 0x7fffffffu; }
+
+// Per-candidate chain |x| maximum: each updating lane has folded the x it read and wrote (x_T .. x_0)
+// into am[]; reduce them per candidate in LDS (amx[CPW], zeroed at kernel start) and store.
+template <int CPW, int THREADS>
+MPCD_DEV void store_chain_absmax(uint32_t *amx, const uint32_t (&am)[2], int cl0, int cl1, bool active, float *out,
+                                 int64_t cand0, int64_t batch)
+{
+    if (active) {
+        atomicMax(amx + cl0, am[0]);
+        if (cl1 >= 0) atomicMax(amx + cl1, am[1]);
+    }
+    lds_barrier();
+    if (threadIdx.x < CPW && cand0 + threadIdx.x < batch)
+        out[cand0 + threadIdx.x] = __builtin_bit_cast(float, amx[threadIdx.x]);
+}
+
 }  // namespace mlpc

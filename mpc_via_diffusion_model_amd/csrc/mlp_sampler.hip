@@ -43,7 +43,8 @@ struct Lds {
     static constexpr int TP = C0 + ROWS * SC0;     // this step's tproj [448]
     static constexpr int BIC = TP + COND_TOTAL;    // biases of the cond layers in tproj column order
     static constexpr int BI = BIC + COND_TOTAL;    // all 14 biases
-    static constexpr int CP = BI + Arch<D0>::btotal();  // per-candidate cproj [CPW][448]
+    static constexpr int AMX = BI + Arch<D0>::btotal();  // uint32 [ROWS]: chain |x| maxima
+    static constexpr int CP = AMX + ROWS;          // per-candidate cproj [CPW][448]
     static constexpr int total(bool ctx) { return CP + (ctx ? CPW * CP_STRIDE : 0); }
 };
 
@@ -219,7 +220,8 @@ struct MlpKernel {
     // final Linear (32 -> D0) in PAIRED mode + the denoise update, x kept in LDS
     static MPCD_DEV void final_and_update(const WFrag<32, D0, PAIRED> &f, const float *__restrict__ bias, float *lds,
                                           const MlpSampleArgs &p, const StepPlan &sp, int s, int64_t cand0,
-                                          const f32x4 (&nz)[WFrag<32, D0, PAIRED>::T][NB], int wave, int lane)
+                                          const f32x4 (&nz)[WFrag<32, D0, PAIRED>::T][NB], uint32_t (&am)[2],
+                                          int wave, int lane)
     {
         constexpr int T = WFrag<32, D0, PAIRED>::T, NT = D0 / 16;
         const int col = lane & 15, q = lane >> 4;
@@ -285,6 +287,7 @@ struct MlpKernel {
                         o = (sp.flags & PLAN_FINAL) ? x0 : x0 * sp.sqan + sp.cn * ec[r];
                     }
                     xn[r] = o;
+                    am[g] = max(am[g], max(abs_bits(xv), abs_bits(o)));  // chain |x| max (x_T .. x_0)
                 }
                 *reinterpret_cast<f32x4 *>(xp) = xn;
                 const int64_t gc = cand0 + cl;
@@ -360,6 +363,8 @@ struct MlpKernel {
                 lds[L::CP + c * CP_STRIDE + k] = gc < p.batch ? p.cproj[(size_t)(p.cproj_stride ? gc : 0) * COND_TOTAL + k] : 0.f;
             }
         }
+        if (threadIdx.x < CPW) reinterpret_cast<uint32_t *>(lds + L::AMX)[threadIdx.x] = 0u;
+        uint32_t am[2] = {0u, 0u};
         // x_T
         for (int i = threadIdx.x; i < CPW * QUADS; i += THREADS) {
             const int c = i / QUADS, qd = i - c * QUADS;
@@ -489,7 +494,12 @@ struct MlpKernel {
             // compiler drain vmcnt(0) at the next use
             load_w(w0, W(0), wave, lane16);
             bar(13);
-            final_and_update(w13, Bs(13), lds, p, cur, s, cand0, nzc, wave, lane);
+            final_and_update(w13, Bs(13), lds, p, cur, s, cand0, nzc, am, wave, lane);
+        }
+        if (SMODE != MODE_EPS && SMODE != MODE_EPS1 && p.chain_absmax) {
+            const int col = lane & 15;
+            store_chain_absmax<CPW, THREADS>(reinterpret_cast<uint32_t *>(lds + L::AMX), am, col, NB == 2 ? -1 : 16 + col,
+                                             true, p.chain_absmax, cand0, p.batch);
         }
 #ifdef MPCD_PROF_LAYERS
         {

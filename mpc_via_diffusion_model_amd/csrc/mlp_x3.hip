@@ -90,7 +90,8 @@ struct Lds3 {
     static constexpr int BIC = TPU + COND_TOTAL * 4;              // fp32 [448]: cond-layer biases
     static constexpr int CPS = BIC + COND_TOTAL * 4;              // fp32 [448]: shared cproj (0 without context)
     static constexpr int BI = CPS + COND_TOTAL * 4;               // fp32 all 14 biases
-    static constexpr int total = BI + Arch<D0>::btotal() * 4;
+    static constexpr int AMX = BI + Arch<D0>::btotal() * 4;       // uint32 [CPW]: chain |x| maxima
+    static constexpr int total = AMX + ROWS * 4;
     static_assert(D0 * 2 + 16 <= RS, "x planes fit a 272-byte row");
 
     // layer l: input / output buffer (byte offset incl. the feature offset of a concat half) and stride
@@ -371,7 +372,8 @@ struct MlpX3 {
 
     // final Linear (32 -> D0) + the denoise update (reference op order, see mlp_sampler.hip)
     static MPCD_DEV void final_and_update(const FW &f, char *lds, const MlpSampleArgs &p, const StepPlan &sp, int s,
-                                          int64_t cand0, const f32x4 (&nz)[NZT][NB], int wave, int lane)
+                                          int64_t cand0, const f32x4 (&nz)[NZT][NB], uint32_t (&am)[2], int wave,
+                                          int lane)
     {
         constexpr int T = FW::T, NT = D0 / 16;
         const int col = lane & 15, q = lane >> 4;
@@ -435,6 +437,8 @@ struct MlpX3 {
                         o = (sp.flags & PLAN_FINAL) ? x0 : x0 * sp.sqan + sp.cn * ec[r];
                     }
                     xn[r] = o;
+                    // chain |x| maximum: the x read here is x_T at s = 0 and every later slice; xn adds x_0
+                    am[g] = max(am[g], max(abs_bits(xv), abs_bits(o)));
                 }
                 store_x(lds, cl, n, xn);
                 if (gc < p.batch) {
@@ -491,6 +495,8 @@ struct MlpX3 {
             for (int i = threadIdx.x; i < A::N[2 * j + 1]; i += THREADS)
                 bic[cond_off(j) + i] = wp[A::woff3(2 * j + 1) + 3 * A::K[2 * j + 1] * A::N[2 * j + 1] / 2 + i];
         for (int i = threadIdx.x; i < COND_TOTAL; i += THREADS) cps[i] = CTX ? p.cproj[i] : 0.f;
+        if (threadIdx.x < CPW) reinterpret_cast<uint32_t *>(lds + L::AMX)[threadIdx.x] = 0u;
+        uint32_t am[2] = {0u, 0u};
         // x_T (fp32 + planes)
         for (int i = threadIdx.x; i < CPW * QUADS; i += THREADS) {
             const int c = i / QUADS, qd = i - c * QUADS;
@@ -603,7 +609,12 @@ struct MlpX3 {
             // next step's layer-0 weights; unconditional (a path-dependent load count drains vmcnt(0))
             load_w3(w0, W(0), wave, lane16);
             bar(13);
-            if (wave < 4) final_and_update(w13, lds, p, cur, s, cand0, nzc, wave, lane);
+            if (wave < 4) final_and_update(w13, lds, p, cur, s, cand0, nzc, am, wave, lane);
+        }
+        if (SMODE != MODE_EPS && SMODE != MODE_EPS1 && p.chain_absmax) {
+            const int col = lane & 15;
+            store_chain_absmax<CPW, THREADS>(reinterpret_cast<uint32_t *>(lds + L::AMX), am, NB == 2 ? col : col,
+                                             NB == 2 ? -1 : 16 + col, wave < 4, p.chain_absmax, cand0, p.batch);
         }
 #ifdef MPCD_PROF_LAYERS
         {

@@ -8,12 +8,12 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <string>
 #include <vector>
 
-#include <rccl/rccl.h>
-
 #include "../../include/mpcd.h"
+#include "comm.h"
 #include "internal.h"
 #include "unet.h"
 
@@ -234,19 +234,23 @@ struct mpcd_ctx {
     // time projections do not depend on the context, so a control loop computes them once)
     std::vector<StepPlan> plan_cached;
     bool plan_cached_valid = false;
+    hipStream_t plan_stream = nullptr;  // stream the cached plan / tproj were produced on
+    hipEvent_t plan_ev = nullptr;       // recorded after they were produced
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     float *dbg = nullptr;  // debug dump target for mpcd_eps (mpcd_debug_set)
-    // candidate-batch data parallelism: one RCCL communicator per context (mpcd_comm_init)
-    ncclComm_t comm = nullptr;
+    // candidate-batch data parallelism: one communicator per context (mpcd_comm_init: RCCL;
+    // mpcd_comm_init_loopback: virtual ranks on one device)
+    Comm *comm = nullptr;
     int nranks = 1, rank = 0;
     // flag: [0] internal clip flag, [16..] zero-initialised counters of the self-resetting reductions
     unsigned *sync_ws() const { return flag.as<unsigned>() + 16; }
     // mpcd_mpc_step: device context row, per-block argmin partials, {best, winner row} result block
     // and its pinned host mirror (one D2H copy per control step)
-    DevBuf step_ctx, step_part, step_out;
+    DevBuf step_ctx, step_part, step_out, step_amax;
     void *step_host = nullptr;
     size_t step_host_bytes = 0;
+    int32_t step_flags = 0;  // mpcd_last_step_flags
 };
 
 namespace {
@@ -475,7 +479,8 @@ int mpcd_create(int device, mpcd_ctx **out)
     HIP_TRY(hipSetDevice(device));
     auto *c = new mpcd_ctx();
     c->device = device;
-    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreateWithFlags(&c->plan_ev, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return fail(MPCD_EHIP, "hipEventCreate failed");
     }
@@ -497,11 +502,12 @@ void mpcd_destroy(mpcd_ctx *c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (DevBuf *b : {&c->params, &c->wpack, &c->wpack3, &c->cond_layers, &c->unet_pack, &c->plan, &c->tproj, &c->cproj, &c->flag,
-                      &c->unet_ws, &c->step_ctx, &c->step_part, &c->step_out})
+                      &c->unet_ws, &c->step_ctx, &c->step_part, &c->step_out, &c->step_amax})
         b->release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
-    if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->plan_ev) (void)hipEventDestroy(c->plan_ev);
+    delete c->comm;
     if (c->step_host) (void)hipHostFree(c->step_host);
     delete c;
 }
@@ -572,6 +578,10 @@ int mpcd_sample(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr)
         HIP_TRY(hipGetLastError());
         c->plan_cached = c->plan_host;
         c->plan_cached_valid = true;
+        c->plan_stream = st;
+        HIP_TRY(hipEventRecord(c->plan_ev, st));
+    } else if (st != c->plan_stream) {  // cached plan / tproj were written on another stream
+        HIP_TRY(hipStreamWaitEvent(st, c->plan_ev, 0));
     }
     const float *cproj = nullptr;
     int64_t cstride = 0;
@@ -597,6 +607,7 @@ int mpcd_sample(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr)
         m.noise = a->noise;
         m.x_out = a->x_out;
         m.chain = a->chain_out;
+        m.chain_absmax = a->chain_absmax;
         m.batch = a->batch;
         m.global_offset = a->global_offset;
         m.seed = a->seed;
@@ -617,6 +628,7 @@ int mpcd_sample(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr)
         u.noise = a->noise;
         u.x_out = a->x_out;
         u.chain = a->chain_out;
+        u.chain_absmax = a->chain_absmax;
         u.batch = a->batch;
         u.global_offset = a->global_offset;
         u.seed = a->seed;
@@ -704,6 +716,29 @@ int mpcd_eps(mpcd_ctx *c, const float *x, int32_t t, const float *context, int32
     m.mode = cfg ? MODE_EPS : MODE_EPS1;
     m.dbg = c->dbg;
     HIP_TRY(launch_mlp(c, m, cfg ? 2 : 1, st));
+    return MPCD_OK;
+}
+
+int mpcd_philox_noise(uint64_t seed, int64_t global_offset, int64_t n_cand, int32_t n_slices, int32_t flat,
+                      float *out, void *stream)
+{
+    if (!out || n_cand < 1 || n_slices < 1 || flat < 4 || flat % 4 || global_offset < 0)
+        return fail(MPCD_EINVAL, "bad mpcd_philox_noise arguments");
+    HIP_TRY(launch_philox_noise(seed, global_offset, n_cand, n_slices, flat, out, static_cast<hipStream_t>(stream)));
+    return MPCD_OK;
+}
+
+int mpcd_last_step_flags(mpcd_ctx *c, int32_t *flags)
+{
+    if (!c || !flags) return fail(MPCD_EINVAL, "null argument");
+    *flags = c->step_flags;
+    return MPCD_OK;
+}
+
+int mpcd_unet_force_tiling(int32_t conv_pick, int32_t block_pick)
+{
+    if (conv_pick < -1 || block_pick < -2) return fail(MPCD_EINVAL, "conv_pick >= -1, block_pick >= -2");
+    unet_force_tiling(conv_pick, block_pick);
     return MPCD_OK;
 }
 
@@ -844,20 +879,12 @@ int mpcd_argmin(mpcd_ctx *c, const double *cost, int64_t n, int64_t offset, mpcd
 
 // ---- candidate-batch data parallelism over RCCL
 
-#define NCCL_TRY(expr)                                                                          \
-    do {                                                                                        \
-        ncclResult_t r_ = (expr);                                                               \
-        if (r_ != ncclSuccess) return fail(MPCD_EHIP, "%s: %s", #expr, ncclGetErrorString(r_)); \
-    } while (0)
-
 int mpcd_comm_unique_id(void *id_out)
 {
     if (!id_out) return fail(MPCD_EINVAL, "null argument");
-    static_assert(sizeof(ncclUniqueId) == MPCD_COMM_ID_BYTES, "ncclUniqueId size");
-    ncclUniqueId id;
-    NCCL_TRY(ncclGetUniqueId(&id));
-    memcpy(id_out, &id, sizeof id);
-    return MPCD_OK;
+    std::string e;
+    int rc = comm_unique_id(id_out, e);
+    return rc ? fail(rc, "%s", e.c_str()) : MPCD_OK;
 }
 
 int mpcd_comm_init(mpcd_ctx *c, int32_t nranks, int32_t rank, const void *id_in)
@@ -865,9 +892,22 @@ int mpcd_comm_init(mpcd_ctx *c, int32_t nranks, int32_t rank, const void *id_in)
     if (!c || !id_in || nranks < 1 || rank < 0 || rank >= nranks) return fail(MPCD_EINVAL, "bad comm arguments");
     if (c->comm) return fail(MPCD_ESTATE, "communicator already initialised");
     HIP_TRY(hipSetDevice(c->device));
-    ncclUniqueId id;
-    memcpy(&id, id_in, sizeof id);
-    NCCL_TRY(ncclCommInitRank(&c->comm, nranks, id, rank));
+    std::string e;
+    int rc = comm_create_rccl(nranks, rank, id_in, &c->comm, e);
+    if (rc) return fail(rc, "%s", e.c_str());
+    c->nranks = nranks;
+    c->rank = rank;
+    return MPCD_OK;
+}
+
+int mpcd_comm_init_loopback(mpcd_ctx *c, int32_t nranks, int32_t rank, uint64_t group_key)
+{
+    if (!c || nranks < 1 || rank < 0 || rank >= nranks) return fail(MPCD_EINVAL, "bad comm arguments");
+    if (c->comm) return fail(MPCD_ESTATE, "communicator already initialised");
+    HIP_TRY(hipSetDevice(c->device));
+    std::string e;
+    int rc = comm_create_loopback(nranks, rank, group_key, &c->comm, e);
+    if (rc) return fail(rc, "%s", e.c_str());
     c->nranks = nranks;
     c->rank = rank;
     return MPCD_OK;
@@ -881,44 +921,53 @@ int mpcd_comm_info(mpcd_ctx *c, int32_t *nranks, int32_t *rank)
     return MPCD_OK;
 }
 
-static int comm_gather(mpcd_ctx *c, const void *send, void *recv, size_t count, ncclDataType_t t, size_t esz,
-                       hipStream_t st)
+static int comm_gather(mpcd_ctx *c, const void *send, void *recv, size_t count, size_t esz, hipStream_t st)
 {
     HIP_TRY(hipSetDevice(c->device));
     if (!c->comm) {  // single rank: the gather is a copy
         if (send != recv) HIP_TRY(hipMemcpyAsync(recv, send, count * esz, hipMemcpyDeviceToDevice, st));
         return MPCD_OK;
     }
-    NCCL_TRY(ncclAllGather(send, recv, count, t, c->comm, st));
-    return MPCD_OK;
+    std::string e;
+    int rc = c->comm->allgather(send, recv, count * esz, st, e);
+    return rc ? fail(rc, "allgather: %s", e.c_str()) : MPCD_OK;
+}
+
+static int comm_reduce(mpcd_ctx *c, void *buf, size_t count, CommOp op, hipStream_t st)
+{
+    if (!c->comm) return MPCD_OK;
+    std::string e;
+    int rc = c->comm->allreduce(buf, count, op, st, e);
+    return rc ? fail(rc, "allreduce: %s", e.c_str()) : MPCD_OK;
 }
 
 int mpcd_allgather_f32(mpcd_ctx *c, const float *send, float *recv, size_t count_per_rank, void *stream)
 {
     if (!c || !send || !recv) return fail(MPCD_EINVAL, "null argument");
-    return comm_gather(c, send, recv, count_per_rank, ncclFloat32, 4, static_cast<hipStream_t>(stream));
+    return comm_gather(c, send, recv, count_per_rank, 4, static_cast<hipStream_t>(stream));
 }
 
 int mpcd_allgather_f64(mpcd_ctx *c, const double *send, double *recv, size_t count_per_rank, void *stream)
 {
     if (!c || !send || !recv) return fail(MPCD_EINVAL, "null argument");
-    return comm_gather(c, send, recv, count_per_rank, ncclFloat64, 8, static_cast<hipStream_t>(stream));
+    return comm_gather(c, send, recv, count_per_rank, 8, static_cast<hipStream_t>(stream));
 }
 
 int mpcd_broadcast_f32(mpcd_ctx *c, float *buf, size_t count, int32_t root, void *stream)
 {
     if (!c || !buf || root < 0 || root >= c->nranks) return fail(MPCD_EINVAL, "bad broadcast arguments");
     HIP_TRY(hipSetDevice(c->device));
-    if (c->comm) NCCL_TRY(ncclBroadcast(buf, buf, count, ncclFloat32, root, c->comm, static_cast<hipStream_t>(stream)));
-    return MPCD_OK;
+    if (!c->comm) return MPCD_OK;
+    std::string e;
+    int rc = c->comm->broadcast(buf, count * 4, root, static_cast<hipStream_t>(stream), e);
+    return rc ? fail(rc, "broadcast: %s", e.c_str()) : MPCD_OK;
 }
 
 int mpcd_allreduce_max_i32(mpcd_ctx *c, int32_t *buf, size_t count, void *stream)
 {
     if (!c || !buf) return fail(MPCD_EINVAL, "null argument");
     HIP_TRY(hipSetDevice(c->device));
-    if (c->comm) NCCL_TRY(ncclAllReduce(buf, buf, count, ncclInt32, ncclMax, c->comm, static_cast<hipStream_t>(stream)));
-    return MPCD_OK;
+    return comm_reduce(c, buf, count, COMM_MAX_I32, static_cast<hipStream_t>(stream));
 }
 
 int mpcd_select(mpcd_ctx *c, const double *cost_local, int64_t n_local, const float *rows_local, int32_t row_len,
@@ -927,12 +976,11 @@ int mpcd_select(mpcd_ctx *c, const double *cost_local, int64_t n_local, const fl
     if (!c || !cost_local || !rows_local || !costs_all || !best_dev || !row_out || n_local < 1 || row_len < 1)
         return fail(MPCD_EINVAL, "bad select arguments");
     hipStream_t st = static_cast<hipStream_t>(stream);
-    int rc = comm_gather(c, cost_local, costs_all, (size_t)n_local, ncclFloat64, 8, st);
+    int rc = comm_gather(c, cost_local, costs_all, (size_t)n_local, 8, st);
     if (rc) return rc;
     HIP_TRY(launch_argmin(costs_all, n_local * c->nranks, 0, best_dev, st));
     HIP_TRY(launch_winner_row(best_dev, (int64_t)c->rank * n_local, n_local, rows_local, row_len, row_out, st));
-    if (c->comm) NCCL_TRY(ncclAllReduce(row_out, row_out, (size_t)row_len, ncclFloat32, ncclSum, c->comm, st));
-    return MPCD_OK;
+    return comm_reduce(c, row_out, (size_t)row_len, COMM_SUM_F32, st);
 }
 
 int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, float *u_best_host, void *stream)
@@ -951,11 +999,13 @@ int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, fl
     if (d.context_dim > 0 && (!a->ctx_min || !a->ctx_max)) return fail(MPCD_EINVAL, "ctx_min / ctx_max");
     if (d.context_dim > 0 && d.context_dim != sys.n_x) return fail(MPCD_EINVAL, "context_dim %d != n_x %d", d.context_dim, sys.n_x);
     if (c->comm && !a->costs_all) return fail(MPCD_EINVAL, "costs_all is required with a communicator");
+    if (a->clip_rule < MPCD_CLIP_CHAIN || a->clip_rule > MPCD_CLIP_NONE) return fail(MPCD_EINVAL, "clip_rule %d", a->clip_rule);
     hipStream_t st = static_cast<hipStream_t>(stream);
     HIP_TRY(hipSetDevice(c->device));
 
     // host staging (pinned): [context row | result block]
-    const size_t out_bytes = sizeof(mpcd_best) + sizeof(float) * (size_t)row;
+    // result block: {best, winner row [row] fp32, clip code int32} - one D2H copy
+    const size_t out_bytes = sizeof(mpcd_best) + sizeof(float) * (size_t)row + sizeof(int32_t);
     const size_t host_bytes = 64 + out_bytes;
     if (c->step_host_bytes < host_bytes) {
         if (c->step_host) (void)hipHostFree(c->step_host);
@@ -982,14 +1032,23 @@ int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, fl
     } else {
         sa.context = nullptr;
     }
+    sa.chain_absmax = nullptr;
+    if (a->clip_rule == MPCD_CLIP_CHAIN) {
+        if ((rc = c->step_amax.ensure(sizeof(float) * (size_t)B))) return rc;
+        sa.chain_absmax = c->step_amax.as<float>();
+    }
     if ((rc = mpcd_sample(c, &sa, stream))) return rc;
 
-    // LimitsNormalizer's global clip flag: provably 0, this rank's own, or the OR over ranks
+    // LimitsNormalizer's global clip flag over the chain (the reference's unnormalize_states of run_CFG's
+    // whole chain), over the final samples, or proven 0; max-reduced over ranks (see mpcd_clip_flag)
     int *flags = c->flag.as<int>();
     const int *flag = flags + 1;  // flag[1] is never written: a constant 0
-    if (!a->flag_zero) {
-        HIP_TRY(launch_clip_flag(sa.x_out, B * row, flags, c->sync_ws(), st));
-        if (c->comm) NCCL_TRY(ncclAllReduce(flags, flags, 1, ncclInt32, ncclMax, c->comm, st));
+    if (a->clip_rule != MPCD_CLIP_NONE) {
+        if (a->clip_rule == MPCD_CLIP_CHAIN)
+            HIP_TRY(launch_clip_flag(sa.chain_absmax, B, flags, c->sync_ws(), st));
+        else
+            HIP_TRY(launch_clip_flag(sa.x_out, B * row, flags, c->sync_ws(), st));
+        if ((rc = comm_reduce(c, flags, 1, COMM_MAX_I32, st))) return rc;
         flag = flags;
     }
     mpcd_best *best_dev = c->step_out.as<mpcd_best>();
@@ -1004,17 +1063,28 @@ int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, fl
         HIP_TRY(launch_rollout_cost(sys, a->x0, nullptr, B, sa.x_out, a->act_min, a->act_max, flag, B, H,
                                     a->cost_local, st));
         float *row_norm = reinterpret_cast<float *>(part_idx + n_part);
-        if ((rc = comm_gather(c, a->cost_local, a->costs_all, (size_t)B, ncclFloat64, 8, st))) return rc;
+        if ((rc = comm_gather(c, a->cost_local, a->costs_all, (size_t)B, 8, st))) return rc;
         HIP_TRY(launch_argmin(a->costs_all, B * c->nranks, 0, best_dev, st));
         HIP_TRY(launch_winner_row(best_dev, (int64_t)c->rank * B, B, sa.x_out, row, row_norm, st));
-        NCCL_TRY(ncclAllReduce(row_norm, row_norm, (size_t)row, ncclFloat32, ncclSum, c->comm, st));
+        if ((rc = comm_reduce(c, row_norm, (size_t)row, COMM_SUM_F32, st))) return rc;
         HIP_TRY(launch_unnormalize(row_norm, row, d.state_dim, flag, a->act_min, a->act_max, u_dev, st));
     }
+    int32_t *code_dev = reinterpret_cast<int32_t *>(u_dev + row);
+    HIP_TRY(hipMemcpyAsync(code_dev, flag, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     void *host_out = static_cast<char *>(c->step_host) + 64;
     HIP_TRY(hipMemcpyAsync(host_out, c->step_out.p, out_bytes, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     memcpy(best_host, host_out, sizeof(mpcd_best));
     memcpy(u_best_host, static_cast<char *>(host_out) + sizeof(mpcd_best), sizeof(float) * (size_t)row);
+    int32_t code = 0;
+    memcpy(&code, static_cast<char *>(host_out) + sizeof(mpcd_best) + sizeof(float) * (size_t)row, sizeof code);
+    c->step_flags = (code == 1 ? MPCD_STEP_CLIPPED : 0) | (code == 2 ? MPCD_STEP_NAN_SAMPLES : 0);
+    if (!std::isfinite(best_host->cost)) {
+        c->step_flags |= MPCD_STEP_NONFINITE_WINNER;
+        return fail(MPCD_ENONFINITE, "mpcd_mpc_step: no candidate has a finite cost (best %g, index %lld)%s",
+                    best_host->cost, (long long)best_host->index,
+                    code == 2 ? "; NaN in the sampled trajectories" : "");
+    }
     return MPCD_OK;
 }
 

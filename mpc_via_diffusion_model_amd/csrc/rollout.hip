@@ -152,30 +152,41 @@ __device__ __forceinline__ void dyn_step(const SysK &S, const double *x, const d
     }
 }
 
-// any |u_norm| outside [-1-eps, 1+eps]  ->  *flag = 1, else 0  (x.max() > 1+eps or x.min() < -1-eps).
-// One launch, no memset: blocks OR into ws[0]; the last block to finish (ws[1] counts them) moves the
-// result to *flag and leaves ws zeroed for the next launch on the stream.
+// LimitsNormalizer's global clip test x.max() > 1+eps or x.min() < -1-eps (normalization.py:160) with
+// torch's NaN semantics: a NaN makes max() and min() NaN, both comparisons false, no clip. Result code:
+// 0 = in range, 1 = clip, 2 = a NaN was seen (no clip; 2 also wins a max-reduction over ranks, as a NaN
+// on any rank makes the global max NaN). Consumers clip iff the flag is exactly 1.
+// One launch, no memset: blocks OR bit0 (out of range) / bit1 (NaN) into ws[0]; the last block to finish
+// (ws[1] counts them) moves the result to *flag and leaves ws zeroed for the next launch on the stream.
+__device__ __forceinline__ unsigned clip_bits(float v, float hi, float lo)
+{
+    return ((v > hi) | (v < lo)) ? 1u : (v != v ? 2u : 0u);
+}
+__device__ __forceinline__ int clip_code(unsigned bits) { return (bits & 2u) ? 2 : (int)(bits & 1u); }
+
 __global__ __launch_bounds__(256) void clip_flag_kernel(const float *x, int64_t n, int *flag, unsigned *ws)
 {
     const float hi = (float)(1.0 + 1e-4), lo = (float)(-1.0 - 1e-4);
-    int any = 0;
+    unsigned any = 0;
     const int64_t n4 = ((uintptr_t)x & 15) ? 0 : n >> 2;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         const f32x4 v = reinterpret_cast<const f32x4 *>(x)[i];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) any |= (v[e] > hi) | (v[e] < lo);
+        for (int e = 0; e < 4; ++e) any |= clip_bits(v[e], hi, lo);
     }
-    for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float v = x[i];
-        any |= (v > hi) | (v < lo);
-    }
-    any = __syncthreads_or(any);
+    for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        any |= clip_bits(x[i], hi, lo);
+    __shared__ unsigned blk;
+    if (threadIdx.x == 0) blk = 0;
+    __syncthreads();
+    if (any) atomicOr(&blk, any);
+    __syncthreads();
     if (threadIdx.x == 0) {
-        if (any) atomicOr(ws, 1u);
+        if (blk) atomicOr(ws, blk);
         __threadfence();
         if (atomicAdd(ws + 1, 1u) == gridDim.x - 1) {
             __threadfence();
-            *flag = (int)atomicExch(ws, 0u);
+            *flag = clip_code(atomicExch(ws, 0u));
             atomicExch(ws + 1, 0u);
         }
     }
@@ -190,7 +201,7 @@ __device__ __forceinline__ float unnorm1(float v, bool clip, float mn, float mx)
 
 __global__ void unnormalize_kernel(const float *x, int64_t n, int dim, const int *flag, const MinMax lim, float *out)
 {
-    const bool clip = *flag != 0;
+    const bool clip = *flag == 1;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int c = (int)(i % dim);
         out[i] = unnorm1(x[i], clip, lim.mn[c], lim.mx[c]);
@@ -227,7 +238,7 @@ __global__ __launch_bounds__(RT_THREADS) void rollout_cost_kernel(const SysK S, 
     }
     __syncthreads();
     const int64_t b = min(c0 + threadIdx.x, batch - 1);  // lanes past the batch recompute the last one
-    const bool clip = flags[b / group] != 0;
+    const bool clip = flags[b / group] == 1;
     float mn[nu], mx[nu];
 #pragma unroll
     for (int i = 0; i < nu; ++i) { mn[i] = S.umin[i]; mx[i] = S.umax[i]; }
@@ -294,22 +305,28 @@ __global__ __launch_bounds__(RT_THREADS) void rollout_cost_kernel(const SysK S, 
             *K.counter = 0u;
         }
         if (i >= 0 && K.row_out) {
-            const bool clip0 = flags[0] != 0;
+            const bool clip0 = flags[0] == 1;
             for (int k = threadIdx.x; k < row; k += RT_THREADS)
                 K.row_out[k] = unnorm1(u_norm[(size_t)i * row + k], clip0, S.umin[k % nu], S.umax[k % nu]);
         }
     }
 }
 
-// Per-group clip flags: flags[g] = any element of x[g*group_elems, (g+1)*group_elems) outside
-// [-1-1e-4, 1+1e-4] (LimitsNormalizer's rule applied to each plant state's own candidate batch).
-__global__ void clip_flags_kernel(const float *x, int64_t n, int64_t group_elems, int *flags)
+// Per-group clip flags: flags[g] = the clip code above over x[g*group_elems, (g+1)*group_elems)
+// (LimitsNormalizer's rule applied to each plant state's own candidate batch). One workgroup per group:
+// every flag is written, so no memset is needed.
+__global__ __launch_bounds__(256) void clip_flags_kernel(const float *x, int64_t group_elems, int *flags)
 {
     const float hi = (float)(1.0 + 1e-4), lo = (float)(-1.0 - 1e-4);
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float v = x[i];
-        if ((v > hi) | (v < lo)) atomicOr(flags + i / group_elems, 1);
-    }
+    const float *g = x + (size_t)blockIdx.x * group_elems;
+    unsigned any = 0;
+    for (int64_t i = threadIdx.x; i < group_elems; i += blockDim.x) any |= clip_bits(g[i], hi, lo);
+    __shared__ unsigned blk;
+    if (threadIdx.x == 0) blk = 0;
+    __syncthreads();
+    if (any) atomicOr(&blk, any);
+    __syncthreads();
+    if (threadIdx.x == 0) flags[blockIdx.x] = clip_code(blk);
 }
 
 // normalize_condition for a batch of plant states (normalization.py:149-154 in fp64, then the net's
@@ -376,7 +393,7 @@ __global__ __launch_bounds__(CS_THREADS) void control_step_kernel(const SysK S, 
     }
     if (threadIdx.x != 0) return;
     const int64_t idx = si[0];
-    const bool clip = flags[m] != 0;
+    const bool clip = flags[m] == 1;
     double x[nx], xn[nx], u[nu];
 #pragma unroll
     for (int i = 0; i < nx; ++i) x[i] = x_dev[m * nx + i];
@@ -524,12 +541,8 @@ hipError_t launch_argmin(const double *cost, int64_t n, int64_t offset, mpcd_bes
 
 hipError_t launch_clip_flags(const float *x, int64_t n_groups, int64_t group_elems, int *flags_dev, hipStream_t stream)
 {
-    hipError_t e = hipMemsetAsync(flags_dev, 0, sizeof(int) * n_groups, stream);
-    if (e != hipSuccess) return e;
-    const int64_t n = n_groups * group_elems;
-    const int64_t blocks = std::min<int64_t>(4096, (n + 255) / 256);
-    hipLaunchKernelGGL(clip_flags_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, stream, x, n,
-                       group_elems, flags_dev);
+    if (n_groups > 0x7fffffff) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(clip_flags_kernel, dim3((unsigned)n_groups), dim3(256), 0, stream, x, group_elems, flags_dev);
     return hipGetLastError();
 }
 

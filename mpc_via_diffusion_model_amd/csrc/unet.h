@@ -59,6 +59,7 @@ struct ConvMK {
     int lds_out, nx_off, nx_cs, nx_win, nx_halo_l;
     // fp16 activation buffers (f16 net): input (xa / xb), residual, output hold halves, not floats
     int in_h, res_h, out_h;
+    int layer;              // index of the conv in UnetWeights::layers (diagnostics)
 };
 
 struct UnetWeights {
@@ -78,6 +79,7 @@ struct UnetSampleArgs {
     const float *noise;
     float *x_out;
     float *chain;
+    float *chain_absmax;           // [B] or null: max |x| over the chain per candidate (mpcd_sample_args)
     int64_t batch;
     int64_t global_offset;
     uint64_t seed;
@@ -105,6 +107,9 @@ hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::
 // + residual, k2.xa = k1.out) as one fused launch when that measures faster than the pair (the
 // intermediate then stays in LDS and k1.out is not written). MPCD_UNET_FUSE=0/1 forces either form.
 hipError_t unet_launch_mx_rtb(int planes, ConvMK &k1, ConvMK &k2, hipStream_t st, std::string *why);
+
+// mpcd_unet_force_tiling (include/mpcd.h)
+void unet_force_tiling(int conv, int block);
 
 using TensorLookup = std::function<const float *(const char *)>;
 

@@ -278,7 +278,7 @@ __global__ void init_x_kernel(float *x, int64_t batch, int flat, const float *no
 // x <- update(x, eps) for one denoise step; same arithmetic as the MLP kernel's update
 __global__ void update_kernel(float *x, const float *eps, int64_t batch, int flat, const StepPlan *plan, int s,
                               int mode, int clamp_x0, float wp1, float wf, const float *noise, uint64_t seed,
-                              int64_t goff, float *chain, float *x_out, int last)
+                              int64_t goff, float *chain, float *x_out, int last, uint32_t *amq)
 {
     const int quads = flat / 4;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -317,8 +317,31 @@ __global__ void update_kernel(float *x, const float *eps, int64_t batch, int fla
         }
     }
     *reinterpret_cast<f32x4 *>(x + off) = o;
+    if (amq) {  // running chain |x| maximum of this quad: x read (x_T at s = 0, then each slice) and written
+        // (elements copied to scalars first: a __builtin_bit_cast of a vector-element subscript compiled to
+        // element 0 for every r)
+        uint32_t m = s == 0 ? 0u : amq[i];
+        const float xe[4] = {xv.x, xv.y, xv.z, xv.w}, oe[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t a = __builtin_bit_cast(uint32_t, xe[r]) & 0x7fffffffu;
+            const uint32_t b = __builtin_bit_cast(uint32_t, oe[r]) & 0x7fffffffu;
+            m = max(m, max(a, b));
+        }
+        amq[i] = m;
+    }
     if (chain) *reinterpret_cast<f32x4 *>(chain + (size_t)(s + 1) * batch * flat + off) = o;
     if (last && x_out != x) *reinterpret_cast<f32x4 *>(x_out + off) = o;
+}
+
+// per-candidate chain |x| maximum from the per-quad running maxima (NaN bits win the integer max)
+__global__ void chain_absmax_kernel(const uint32_t *amq, int64_t batch, int quads, float *out)
+{
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= batch) return;
+    uint32_t m = 0;
+    for (int q = 0; q < quads; ++q) m = max(m, amq[b * quads + q]);
+    out[b] = __builtin_bit_cast(float, m);
 }
 
 int group_norm_n_groups(int c)  // layers.py:389-395
@@ -646,6 +669,7 @@ ConvMK make_mk(const Ctx &c, const ConvLayer &L, int epi, const float *xa, int c
     k.in_h = c.is_h(xa);
     k.res_h = c.is_h(res);
     k.out_h = c.is_h(out);
+    k.layer = (int)(&L - c.W->layers.data());
     return k;
 }
 
@@ -805,7 +829,8 @@ int forward(Ctx &c, const Dims &m, Buffers &B, const float *x, int64_t x_rows)
 size_t unet_workspace_bytes(const mpcd_net_desc &d, int64_t batch, int nb)
 {
     const Dims m = dims_of(d);
-    return sizeof(float) * (ws_floats(m, batch * nb) + (size_t)batch * m.H * m.d);
+    // + the sampler state x [B][H][d] and the per-quad chain |x| maxima [B][H*d/4]
+    return sizeof(float) * (ws_floats(m, batch * nb) + (size_t)batch * m.H * m.d + (size_t)batch * (m.H * m.d / 4 + 1));
 }
 
 int unet_sample(const mpcd_net_desc &d, const UnetWeights &W, const UnetSampleArgs &a, hipStream_t st)
@@ -845,6 +870,7 @@ int unet_sample(const mpcd_net_desc &d, const UnetWeights &W, const UnetSampleAr
             return uerr(MPCD_EHIP, "copy eps");
         return MPCD_OK;
     }
+    uint32_t *amq = a.chain_absmax ? reinterpret_cast<uint32_t *>(xs + (size_t)a.batch * flat) : nullptr;
     hipLaunchKernelGGL(init_x_kernel, dim3(g1), dim3(threads), 0, st, xs, a.batch, flat, a.noise, a.seed,
                        a.global_offset, a.chain);
     for (int s = 0; s < a.n_steps; ++s) {
@@ -853,8 +879,11 @@ int unet_sample(const mpcd_net_desc &d, const UnetWeights &W, const UnetSampleAr
         if (rc) return rc;
         hipLaunchKernelGGL(update_kernel, dim3(g1), dim3(threads), 0, st, xs, B.eps, a.batch, flat, a.plan, s, a.mode,
                            a.clamp_x0, a.wp1, a.wf, a.noise, a.seed, a.global_offset, a.chain, a.x_out,
-                           s == a.n_steps - 1 ? 1 : 0);
+                           s == a.n_steps - 1 ? 1 : 0, amq);
     }
+    if (amq)
+        hipLaunchKernelGGL(chain_absmax_kernel, dim3((unsigned)((a.batch + 255) / 256)), dim3(256), 0, st, amq, a.batch,
+                           flat / 4, a.chain_absmax);
     if (hipGetLastError() != hipSuccess) return uerr(MPCD_EHIP, "update launch");
     return MPCD_OK;
 }

@@ -21,6 +21,8 @@
 // through LDS (reusing the staged input when one job per wave suffices) for the GroupNorm statistics
 // (fp64, shifted) and the elementwise epilogue, stored coalesced channels-last.
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -548,6 +550,11 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
                         const float scale = rstd * gw_t[e];
                         const float shift = -scale * mean + gb_t[e];
                         v[e] = mish(raw[e] * scale + shift);
+                        // Keep each element's Mish in scalar VALU ops: when hipcc (ROCm 7.2) packs the four
+                        // elements into v_pk_{mul,fma}_f32, GroupNorm layers gave wrong, run-to-run varying rows
+                        // whenever two workgroups shared a CU (tests/test_gpu_unet_bench_sizes.py); this empty
+                        // register fence after every element removes them at ~2 % of the kernel's time.
+                        asm volatile("" : "+v"(v[e]));
                     }
                     if (epi == UEPI_GN_MISH_COND) {  // row < b_cand: context branch; else the masked (CFG) branch
                         int64_t cand = grow, br = 0;  // branch = row / b_cand (0: context, 1: masked)
@@ -743,6 +750,9 @@ struct MxKey {
 };
 std::mutex g_mx_mu;
 std::map<MxKey, MxChoice> g_mx_cache;  // measured pick per layer shape and batch (process-wide)
+// mpcd_unet_force_tiling: -1 = measured picks; conv >= 0: candidate (conv mod count) of every conv launch;
+// block -2 = never fuse, >= 0: fused candidate (block mod count) of every fusable block
+std::atomic<int> g_force_conv{-1}, g_force_block{-1};
 
 bool autotune_on()
 {
@@ -762,8 +772,9 @@ bool tune_log()  // MPCD_UNET_TUNE_LOG=1: print every measured candidate (stderr
     return on;
 }
 
-hipError_t launch_choice(int kind, int planes, ConvMK &k, const MxChoice &ch, hipStream_t st)
+hipError_t launch_choice(int kind, int planes, ConvMK &k, const MxChoice &ch0, hipStream_t st)
 {
+    const MxChoice &ch = ch0;
     k.rb = ch.rb;
     k.alias = ch.alias;
     k.stat_off = ch.stat_off;
@@ -930,6 +941,20 @@ hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::
     const MxKey key{kind, planes, k.ca, k.cb, k.cout, k.lin, k.lout, k.epi, k.rows, k.x_rows};
     MxChoice pick = cands[0];
     bool have = false;
+    if (int f = g_force_conv.load(); f >= 0) {  // forced candidate (tests: every tiling gives the same bits)
+        // diagnostics: MPCD_UNET_FORCE_LAYER=l applies the forced index to conv l only, the others take
+        // MPCD_UNET_FORCE_BASE (default 0)
+        const char *ol = getenv("MPCD_UNET_FORCE_LAYER"), *ob = getenv("MPCD_UNET_FORCE_BASE");
+        const int only = ol && ol[0] ? atoi(ol) : -1, base = ob && ob[0] ? atoi(ob) : 0;
+        if (only >= 0 && k.layer != only) f = base;
+        const MxChoice &ch = cands[f % cands.size()];
+        if (tune_log() && only >= 0 && k.layer == only)
+            fprintf(stderr, "[mx force] layer %d kind %d P%d cin %d+%d cout %d L %d->%d epi %d rows %lld: rb %d tile %dx%d %s lds %zu\n",
+                    k.layer, kind, planes, k.ca, k.cb, k.cout, k.lin, k.lout, k.epi, (long long)k.rows, ch.rb, ch.t.nn,
+                    ch.t.nc, ch.pers ? "pers" : ch.alias ? "alias" : "tile", ch.lds);
+        k.skip = 0;
+        return launch_choice(kind, planes, k, ch, st);
+    }
     {
         std::lock_guard<std::mutex> g(g_mx_mu);
         auto it = g_mx_cache.find(key);
@@ -1040,6 +1065,12 @@ hipError_t launch_rtb_choice(int planes, const ConvMK &k1, const ConvMK &k2, con
 
 }  // namespace
 
+void unet_force_tiling(int conv, int block)
+{
+    g_force_conv.store(conv < 0 ? -1 : conv);
+    g_force_block.store(block < -2 ? -1 : block);
+}
+
 hipError_t unet_launch_mx_rtb(int planes, ConvMK &k1, ConvMK &k2, hipStream_t st, std::string *why)
 {
     auto unfused = [&]() -> hipError_t {
@@ -1048,7 +1079,8 @@ hipError_t unet_launch_mx_rtb(int planes, ConvMK &k1, ConvMK &k2, hipStream_t st
     };
     const char *fe = getenv("MPCD_UNET_FUSE");  // 0: never fuse, 1: fuse whenever a tiling fits, unset: measured
     const int mode = fe && fe[0] ? atoi(fe) : -1;
-    if (mode == 0) return unfused();
+    const int fb = g_force_block.load();
+    if (mode == 0 || fb == -2 || (fb == -1 && g_force_conv.load() >= 0)) return unfused();
     hipError_t e = prep_geom(UCONV_SAME5, k1, why);
     if (e == hipSuccess) e = prep_geom(UCONV_SAME5, k2, why);
     if (e != hipSuccess) return e;
@@ -1092,6 +1124,7 @@ hipError_t unet_launch_mx_rtb(int planes, ConvMK &k1, ConvMK &k2, hipStream_t st
         return MxKey{UCONV_SAME5, planes, k.ca, k.cb, k.cout, k.lin, k.lout, k.epi, k.rows, k.x_rows};
     };
     const RtbKey key{key_of(k1), key_of(k2)};
+    if (fb >= 0) return launch_rtb_choice(planes, k1, k2, cands[fb % cands.size()], st);
     RtbChoice pick = cands[0];
     bool have = false;
     {

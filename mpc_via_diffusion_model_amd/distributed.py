@@ -61,7 +61,8 @@ def broadcast_row(row_local, owner, group=None):
 
 
 def any_flag(flag_local, group=None):
-    """Logical OR of a per-rank int flag (the global unnormalise clip rule across shards)."""
+    """Max over ranks of a per-rank clip code (mpcd_clip_flag: 0 in range, 1 clip, 2 NaN seen), i.e. the
+    global unnormalise clip rule across shards."""
     rank, size = world(group)
     if size == 1:
         return flag_local
@@ -84,16 +85,23 @@ def select(cost_local, rows_local, argmin, group=None):
 
 
 class NativeComm:
-    """RCCL communicator owned by a planner's libmpcd context (one process per GPU). Rank 0 creates the
-    128-byte unique id; it is shipped to the other ranks over the torch.distributed group (any backend).
-    Without an initialised process group (or with one rank) no communicator is made and the calls
-    reduce to their single-rank forms inside the library."""
+    """Communicator owned by a planner's libmpcd context. Default: RCCL, one process per GPU; rank 0
+    creates the 128-byte unique id, shipped to the other ranks over the torch.distributed group (any
+    backend). Without an initialised process group (or with one rank) no communicator is made and the
+    calls reduce to their single-rank forms inside the library.
+    loopback=(nranks, rank, key): a virtual rank of an in-process loopback group instead (mpcd.h
+    mpcd_comm_init_loopback): nranks planners on the same GPU, each driven by its own host thread,
+    run the N-rank exchange through device copies - the single-GPU test of the RCCL code path."""
 
-    def __init__(self, plan, group=None):
+    def __init__(self, plan, group=None, loopback=None):
         self.plan, self.group = plan, group
-        self.rank, self.size = world(group)
         L = N.lib()
-        if self.size > 1:
+        if loopback is not None:
+            self.size, self.rank, key = (int(v) for v in loopback)
+            N.check(L.mpcd_comm_init_loopback(plan._ctx, self.size, self.rank, key), "mpcd_comm_init_loopback")
+        else:
+            self.rank, self.size = world(group)
+        if self.size > 1 and loopback is None:
             uid = (ctypes.c_uint8 * N.MPCD_COMM_ID_BYTES)()
             if self.rank == 0:
                 N.check(L.mpcd_comm_unique_id(uid), "mpcd_comm_unique_id")
@@ -104,7 +112,7 @@ class NativeComm:
             N.check(L.mpcd_comm_init(plan._ctx, self.size, self.rank, uid), "mpcd_comm_init")
         nr, rk = ctypes.c_int32(), ctypes.c_int32()
         N.check(L.mpcd_comm_info(plan._ctx, ctypes.byref(nr), ctypes.byref(rk)), "mpcd_comm_info")
-        assert (nr.value, rk.value) == ((self.size, self.rank) if self.size > 1 else (1, 0))
+        assert (nr.value, rk.value) == ((self.size, self.rank) if self.size > 1 or loopback else (1, 0))
         self._best = torch.zeros(2, dtype=torch.float64, device=plan.device)
 
     def any_flag(self, flag_local):

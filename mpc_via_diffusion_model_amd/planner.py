@@ -27,8 +27,27 @@ from . import schedule as S
 from .systems import System
 
 _STEP_CONTEXT = object()  # _args placeholder: mpcd_mpc_step normalises x0 into the context itself
+_CLIP_RULES = {"chain": N.MPCD_CLIP_CHAIN, "final": N.MPCD_CLIP_FINAL}
 _SAMPLERS = {"ddpm_cfg": N.MPCD_DDPM_CFG, "ddpm_cart_pole_sample_fn": N.MPCD_DDPM_CFG,
              "ddim_cfg": N.MPCD_DDIM_CFG, "ddim": N.MPCD_DDIM, "ddim_sample": N.MPCD_DDIM}
+
+
+def philox_noise(n_cand, n_slices, flat, seed=0, global_offset=0, device=None):
+    """The samplers' in-kernel noise for candidates [global_offset, global_offset + n_cand) as a device
+    tensor [n_slices, n_cand, flat] (slice 0 = x_T, slice k = denoise step k's draw): feeding it back as
+    `noise` replays a Philox run in injected-noise mode (mpcd_philox_noise)."""
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+    out = torch.empty((int(n_slices), int(n_cand), int(flat)), dtype=torch.float32, device=dev)
+    N.check(N.lib().mpcd_philox_noise(int(seed) & 0xFFFFFFFFFFFFFFFF, int(global_offset), int(n_cand), int(n_slices),
+                                      int(flat), ctypes.c_void_p(out.data_ptr()),
+                                      ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "mpcd_philox_noise")
+    return out
+
+
+def force_unet_tiling(conv=-1, block=-1):
+    """Process-wide U-Net tiling override (mpcd_unet_force_tiling): conv = candidate index for every conv
+    (-1: measured), block = fused-block candidate (-1: measured, -2: never fuse)."""
+    N.check(N.lib().mpcd_unet_force_tiling(int(conv), int(block)), "mpcd_unet_force_tiling")
 
 
 @dataclass
@@ -70,6 +89,7 @@ class MPCResult:
     best_index: int         # global candidate index
     costs: torch.Tensor     # [B_total] fp64 on device (all ranks' candidates)
     u_norm: torch.Tensor    # [B_local, H, d] this rank's normalised samples
+    flags: int = 0          # mpcd_last_step_flags bits (native step): 1 clipped, 2 NaN in the samples
 
 
 @dataclass
@@ -117,7 +137,8 @@ class DiffusionMPC:
         N.check(self._lib.mpcd_set_schedule(self._ctx, ctypes.c_void_p(tab.data_ptr()), self.n_steps,
                                             ctypes.c_void_p(std.data_ptr())), "mpcd_set_schedule")
         # DDPM with clip_denoised ends with x = coef1[0]*clamp(x0) + coef2[0]*x: if coef2[0] == 0 and
-        # |coef1[0]| <= 1 + 1e-4 the unnormalise clip flag is provably 0 for every candidate.
+        # |coef1[0]| <= 1 + 1e-4 the clip flag over the FINAL samples is provably 0 (clip_rule="final";
+        # the reference's chain-wide rule still sees x_T and is computed).
         c1, c2 = float(self.tables["posterior_mean_coef1"][0]), float(self.tables["posterior_mean_coef2"][0])
         self.ddpm_final_in_range = c2 == 0.0 and abs(c1) <= np.float32(1 + 1e-4)
         self._flag = torch.zeros(1, dtype=torch.int32, device=self.device)
@@ -176,7 +197,7 @@ class DiffusionMPC:
         return _SAMPLERS[name]
 
     def _args(self, sampler, batch, context, w, n_wo_noise, ddim_steps, clamp_x0, seed, global_offset, noise,
-              x_out, chain):
+              x_out, chain, absmax=None):
         a = N.SampleArgs()
         if self.spec.context_dim > 0 and context is not _STEP_CONTEXT:
             if context is None:
@@ -201,6 +222,7 @@ class DiffusionMPC:
         a.noise = noise.data_ptr() if noise is not None else None
         a.x_out = x_out.data_ptr()
         a.chain_out = chain.data_ptr() if chain is not None else None
+        a.chain_absmax = absmax.data_ptr() if absmax is not None else None
         return a
 
     def n_denoise_steps(self, sample_fn="ddpm_cfg", n_wo_noise=0, ddim_steps=None):
@@ -219,9 +241,12 @@ class DiffusionMPC:
 
     def sample_trajectories(self, context=None, n_samples=1, horizon=None, w=0.01, sample_fn="ddpm_cfg",
                             n_wo_noise=0, ddim_steps=None, clamp_x0=False, seed=0, global_offset=0, noise=None,
-                            return_chain=False, out=None):
+                            return_chain=False, out=None, absmax_out=None):
         """Normalised candidate trajectories [B, H, d] (or the chain [S+1, B, H, d]).
-        context: [1, C] (shared) or [B, C] normalised fp32; noise: optional injected [S+1, B, H, d]."""
+        context: [1, C] (shared) or [B, C] normalised fp32; noise: optional injected [S+1, B, H, d].
+        absmax_out: optional fp32 [B] device tensor <- per candidate max |x| over the whole chain
+        (x_T .. x_0; NaN if any NaN): the input of the reference's chain-wide clip test without
+        materialising the chain."""
         H = horizon or self.spec.horizon
         if H != self.spec.horizon:
             raise ValueError(f"net was built for horizon {self.spec.horizon}")
@@ -240,7 +265,11 @@ class DiffusionMPC:
                 raise ValueError(f"noise must be [{steps + 1}, {B}, {H}, {d}], got {tuple(noise.shape)}")
         x = out if out is not None else torch.empty((B, H, d), dtype=torch.float32, device=self.device)
         chain = torch.empty((steps + 1, B, H, d), dtype=torch.float32, device=self.device) if return_chain else None
-        a = self._args(sampler, B, context, w, n_wo_noise, ddim_steps, clamp_x0, seed, global_offset, noise, x, chain)
+        if absmax_out is not None and (absmax_out.dtype != torch.float32 or absmax_out.numel() != B
+                                       or absmax_out.device != self.device or not absmax_out.is_contiguous()):
+            raise ValueError(f"absmax_out must be a contiguous fp32 [{B}] tensor on {self.device}")
+        a = self._args(sampler, B, context, w, n_wo_noise, ddim_steps, clamp_x0, seed, global_offset, noise, x, chain,
+                       absmax_out)
         N.check(self._lib.mpcd_sample(self._ctx, ctypes.byref(a), self._stream()), "mpcd_sample")
         return chain if return_chain else x
 
@@ -305,7 +334,8 @@ class DiffusionMPC:
         return int(host.view(torch.int64)[1]), float(host[0])
 
     def closed_loop(self, x0_states, system: System, iterations, n_samples=1, w=0.01, sample_fn="ddpm_cfg",
-                    n_wo_noise=0, ddim_steps=None, clamp_x0=False, select="argmin", decimals=4, seed=0, noise=None):
+                    n_wo_noise=0, ddim_steps=None, clamp_x0=False, select="argmin", decimals=4, seed=0, noise=None,
+                    clip_rule="chain"):
         """Closed-loop diffusion MPC for M plant states at once, resident on the device.
         The reference runs one initial state at a time on the host (Cart_Diffusion_inference.py:405-512:
         normalize_condition -> run_CFG -> unnormalize -> u0 = round(u[0], 4) -> x = f(x, u0), repeated
@@ -315,9 +345,13 @@ class DiffusionMPC:
         nothing returns to the host until the end. select: "argmin" (lowest cost) or "first" (candidate 0 of
         each group: the reference scripts with n_samples = 1). Per-state contexts use the exact-f32 MLP
         kernel (the split-bf16 one needs a shared context). noise: optional callable it -> injected sampler
-        noise [S+1, M*n_samples, H, d] (parity tests); default in-kernel Philox keyed by (seed + it)."""
+        noise [S+1, M*n_samples, H, d] (parity tests); default in-kernel Philox keyed by (seed + it).
+        clip_rule: "chain" (the reference: run_CFG(return_chain=True) then unnormalize_states of the whole
+        chain, so each state's clip test also sees its x_T) or "final" (the final samples only)."""
         if select not in ("argmin", "first"):
             raise ValueError("select must be 'argmin' or 'first'")
+        if clip_rule not in _CLIP_RULES:
+            raise ValueError(f"clip_rule must be one of {sorted(_CLIP_RULES)}")
         x0 = np.ascontiguousarray(np.atleast_2d(np.asarray(x0_states, dtype=np.float64)))
         M, nx = x0.shape
         if nx != system.n_x or system.n_u != self.spec.state_dim:
@@ -337,14 +371,19 @@ class DiffusionMPC:
         flags = torch.empty(M, dtype=torch.int32, device=dev)
         cost = torch.empty(B, dtype=torch.float64, device=dev)
         u_norm = torch.empty((B, H, d), dtype=torch.float32, device=dev)
+        absmax = torch.empty(B, dtype=torch.float32, device=dev) if clip_rule == "chain" else None
         ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         xs[0] = x
         for it in range(T):
             N.check(self._lib.mpcd_normalize_states(self._ctx, ptr(x), M, nx, self.ctx_min.ctypes.data,
                                                     self.ctx_max.ctypes.data, ptr(ctx), st), "mpcd_normalize_states")
             self.sample_trajectories(ctx.repeat_interleave(n, dim=0), B, H, w, sample_fn, n_wo_noise, ddim_steps,
-                                     clamp_x0, seed + it, 0, None if noise is None else noise(it), False, out=u_norm)
-            N.check(self._lib.mpcd_clip_flags(self._ctx, ptr(u_norm), M, n * H * d, ptr(flags), st), "mpcd_clip_flags")
+                                     clamp_x0, seed + it, 0, None if noise is None else noise(it), False, out=u_norm,
+                                     absmax_out=absmax)
+            if absmax is not None:  # each state's flag over its candidates' chains
+                N.check(self._lib.mpcd_clip_flags(self._ctx, ptr(absmax), M, n, ptr(flags), st), "mpcd_clip_flags")
+            else:
+                N.check(self._lib.mpcd_clip_flags(self._ctx, ptr(u_norm), M, n * H * d, ptr(flags), st), "mpcd_clip_flags")
             N.check(self._lib.mpcd_rollout_cost_grouped(self._ctx, ctypes.byref(desc), ptr(x), n, ptr(u_norm),
                                                         self.act_min.ctypes.data, self.act_max.ctypes.data, B, H,
                                                         ptr(flags), ptr(cost), st), "mpcd_rollout_cost_grouped")
@@ -357,35 +396,47 @@ class DiffusionMPC:
                                 cost=cs.t().cpu().numpy(), index=ix.t().cpu().numpy())
 
     def mpc_step(self, x0, system: System, n_samples, w=0.01, sample_fn="ddpm_cfg", n_wo_noise=0, ddim_steps=None,
-                 clamp_x0=False, seed=0, noise=None, group=None, comm=None, native=None):
+                 clamp_x0=False, seed=0, noise=None, group=None, comm=None, native=None, clip_rule="chain"):
         """One control step: sample n_samples candidates on this rank (weak scaling: every rank adds
         n_samples), roll out + cost them, all-gather costs, pick the global argmin, broadcast it.
         comm: a distributed.NativeComm (the exchange inside libmpcd.so over RCCL) or None
         (torch.distributed collectives on `group`).
         native: run the whole step as one mpcd_mpc_step call (default whenever the library can do the
         exchange itself: a NativeComm, or a single rank); False = the step composed from the separate
-        entry points (sample, clip flag, rollout, select), kept as the reference composition."""
-        rank, size = D.world(group)
+        entry points (sample, clip flag, rollout, select), kept as the reference composition.
+        clip_rule: which tensor LimitsNormalizer's global clip test runs over. "chain" (default) = the
+        reference scripts, which call run_CFG(return_chain=True) and unnormalise the whole chain
+        (Cart_Diffusion_inference.py:450-463, Diffusion_MPC_Inference.py:232-247), so x_T ~ N(0, 1) is in
+        the test; "final" = the final samples only (proven 0 for DDPM when the last posterior mean cannot
+        leave [-1, 1], then no reduction is run)."""
+        if clip_rule not in _CLIP_RULES:
+            raise ValueError(f"clip_rule must be one of {sorted(_CLIP_RULES)}")
+        if comm is not None:
+            rank, size = comm.rank, comm.size
+        else:
+            rank, size = D.world(group)
         if native is None:
             native = comm is not None or size == 1
         if native:
             if size > 1 and comm is None:
                 raise ValueError("native mpc_step on several ranks needs a NativeComm")
             return self._mpc_step_native(x0, system, n_samples, w, sample_fn, n_wo_noise, ddim_steps, clamp_x0, seed,
-                                         noise, comm)
-        offset, total = D.shard(n_samples, group)
-        ctx = torch.from_numpy(self.normalize_condition(x0)[None])
+                                         noise, comm, clip_rule)
+        offset = rank * n_samples
+        ctx = torch.from_numpy(self.normalize_condition(x0)[None]) if self.spec.context_dim > 0 else None
+        absmax = torch.empty(n_samples, dtype=torch.float32, device=self.device) if clip_rule == "chain" else None
         u_norm = self.sample_trajectories(ctx, n_samples, self.spec.horizon, w, sample_fn, n_wo_noise, ddim_steps,
-                                          clamp_x0, seed, offset, noise)
-        # LimitsNormalizer's clip flag is global over the whole batch: one rank's own flag, the OR
-        # over ranks, or provably zero (DDPM whose last posterior mean stays in range) -> no exchange
+                                          clamp_x0, seed, offset, noise, absmax_out=absmax)
+        # LimitsNormalizer's clip flag is global over the whole batch: this rank's own code, the max over
+        # ranks (mpcd_clip_flag codes: 1 = clip, 2 = NaN seen), or provably zero (final-samples rule,
+        # DDPM whose last posterior mean stays in range) -> no exchange
         sampler = self._sampler_id(sample_fn)
-        if size == 1:
-            flag = self.clip_flag(u_norm)
-        elif sampler == N.MPCD_DDPM_CFG and self.ddpm_final_in_range:
+        if clip_rule == "final" and sampler == N.MPCD_DDPM_CFG and self.ddpm_final_in_range:
             flag = torch.zeros(1, dtype=torch.int32, device=self.device)
         else:
-            flag = comm.any_flag(self.clip_flag(u_norm)) if comm else D.any_flag(self.clip_flag(u_norm), group)
+            flag = self.clip_flag(absmax if absmax is not None else u_norm)
+            if size > 1:
+                flag = comm.any_flag(flag) if comm else D.any_flag(flag, group)
         cost_local = self.rollout_cost(system, x0, u_norm, flag)
         if comm is not None:
             idx, best, row, costs = comm.select(cost_local, u_norm)
@@ -397,7 +448,7 @@ class DiffusionMPC:
                          u_norm=u_norm)
 
     def _mpc_step_native(self, x0, system, n_samples, w, sample_fn, n_wo_noise, ddim_steps, clamp_x0, seed, noise,
-                         comm):
+                         comm, clip_rule="chain"):
         """mpc_step as one libmpcd call (mpcd_mpc_step): one H2D copy of the context row, the kernels,
         one D2H copy of {best, u_best}, one stream synchronisation."""
         size, rank = (comm.size, comm.rank) if comm is not None else (1, 0)
@@ -422,12 +473,17 @@ class DiffusionMPC:
         a.act_min, a.act_max = self.act_min.ctypes.data, self.act_max.ctypes.data
         a.sample = self._args(sampler, B, _STEP_CONTEXT, w, n_wo_noise, ddim_steps, clamp_x0, seed, rank * B, noise,
                               u_norm, None)
-        a.flag_zero = 1 if (sampler == N.MPCD_DDPM_CFG and self.ddpm_final_in_range) else 0
+        a.clip_rule = _CLIP_RULES[clip_rule]
+        if clip_rule == "final" and sampler == N.MPCD_DDPM_CFG and self.ddpm_final_in_range:
+            a.clip_rule = N.MPCD_CLIP_NONE
         a.cost_local = cost.data_ptr()
         a.costs_all = costs.data_ptr()
         best = N.Best()
         u_best = np.empty((H, d), dtype=np.float32)
+        # MPCD_ENONFINITE (no candidate with a finite cost: NaN / Inf samples) raises MpcdError here
         N.check(self._lib.mpcd_mpc_step(self._ctx, ctypes.byref(a), ctypes.byref(best), u_best.ctypes.data,
                                         self._stream()), "mpcd_mpc_step")
+        fl = ctypes.c_int32()
+        N.check(self._lib.mpcd_last_step_flags(self._ctx, ctypes.byref(fl)), "mpcd_last_step_flags")
         return MPCResult(u0=u_best[0].copy(), u_best=u_best, best_cost=best.cost, best_index=best.index, costs=costs,
-                         u_norm=u_norm)
+                         u_norm=u_norm, flags=fl.value)

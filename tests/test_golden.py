@@ -56,7 +56,9 @@ def test_gpu_matches_golden(name):
     ref = torch.from_numpy(fx["chain"])
     assert_traj_close(chain[: ref.shape[0]], ref, what=name)
     cost = plan.rollout_cost(systems.get(c["system"]), fx["x0"], chain[ref.shape[0] - 1]).cpu().numpy()
-    np.testing.assert_allclose(cost, fx["cost"], rtol=1e-3)
+    # SURVEY §8d bar. Measured amplification of sampler rounding into these costs (oracle with fp64 GEMMs vs
+    # the fixtures): <= 3.5e-6 relative (DDIM), <= 3e-8 (DDPM), so 1e-4 is the bar, not a loosened one
+    np.testing.assert_allclose(cost, fx["cost"], rtol=1e-4)
     idx, _ = plan.argmin(torch.from_numpy(cost).cuda())
     i = int(fx["best"])
     assert idx == i or abs(fx["cost"][idx] - fx["cost"][i]) <= 1e-4 * abs(fx["cost"][i])

@@ -21,11 +21,12 @@ def _oracle_closed_loop(net, bufs, x0, sysname, T, n, H, d, w, noise, cmin, cmax
     xs, us, idx = [x.copy()], [], []
     for it in range(T):
         ctx = onorm.normalize(torch.from_numpy(x), torch.from_numpy(cmin), torch.from_numpy(cmax)).float()
-        un = osam.ddpm_cfg(net, bufs, ctx.repeat_interleave(n, 0), w, M * n, H, noise=noise(it))
+        chain = osam.ddpm_cfg(net, bufs, ctx.repeat_interleave(n, 0), w, M * n, H, noise=noise(it), return_chain=True)
         u_it, i_it = [], []
         for m in range(M):
-            g = un[m * n:(m + 1) * n]
-            u = onorm.unnormalize(g, torch.from_numpy(amin), torch.from_numpy(amax))
+            # run_CFG(return_chain=True) -> unnormalize_states(chain)[-1] (Cart_Diffusion_inference.py:450-465)
+            g = chain[:, m * n:(m + 1) * n]
+            u = onorm.unnormalize(g, torch.from_numpy(amin), torch.from_numpy(amax))[-1]
             cost = osys.rollout_cost(sysname, x[m], u.double().numpy())
             i = 0 if select == "first" else int(osys.argmin(cost))
             u0 = np.array([round(float(v), 4) for v in u[i, 0]], dtype=np.float64)

@@ -1,4 +1,6 @@
 """GPU parity: fp64 rollout/cost kernel vs the C oracle, unnormalise clip rule, argmin, mpc_step."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -8,7 +10,7 @@ from oracle import sampler as osam
 from oracle import schedule as osch
 from oracle import systems as osys
 
-from ._util import make_mlp, unnormalize_np
+from ._util import make_mlp, make_unet, unnormalize_np
 
 pytestmark = pytest.mark.gpu
 
@@ -108,15 +110,22 @@ def test_mpc_step_matches_oracle_pipeline(native, B):
     x0 = np.array([0.3, 0.1, 0.95 * np.pi, -0.2, red(0.95 * np.pi)])
     noise = torch.randn(N + 1, B, H, d, generator=torch.Generator().manual_seed(1))
     res = plan.mpc_step(x0, systems.cartpole_lin5(), B, w=0.01, noise=noise, native=native)
-    # oracle pipeline
+    # oracle pipeline: run_CFG(return_chain=True) -> unnormalize_states(chain) -> chain[-1]
+    # (Cart_Diffusion_inference.py:450-465: the clip test sees the whole chain, x_T included)
     from oracle import normalizer as onorm
     ctx = onorm.normalize(torch.from_numpy(x0)[None], torch.from_numpy(cmin), torch.from_numpy(cmax)).float()
-    x = osam.ddpm_cfg(net, osch.buffers("exponential", N), ctx.expand(B, C), 0.01, B, H, noise=noise)
-    u = onorm.unnormalize(x, torch.from_numpy(lo.astype(np.float32)), torch.from_numpy(hi.astype(np.float32)))
+    chain = osam.ddpm_cfg(net, osch.buffers("exponential", N), ctx.expand(B, C), 0.01, B, H, noise=noise,
+                          return_chain=True)
+    u = onorm.unnormalize(chain, torch.from_numpy(lo.astype(np.float32)), torch.from_numpy(hi.astype(np.float32)))[-1]
     cost = osys.rollout_cost("cartpole_lin5", x0, u.double().numpy())
     i = osys.argmin(cost)
     gpu_cost = res.costs.cpu().numpy()
-    np.testing.assert_allclose(gpu_cost, cost, rtol=1e-3)
+    # the cost kernel is bit-exact on the GPU's own samples (clipped, as the chain rule says)
+    u_gpu = np.clip(res.u_norm.cpu().numpy(), np.float32(-1), np.float32(1))
+    u_gpu = ((u_gpu + np.float32(1)) / np.float32(2)) * (hi - lo).astype(np.float32) + lo.astype(np.float32)
+    np.testing.assert_array_equal(gpu_cost, osys.rollout_cost("cartpole_lin5", x0, u_gpu.astype(np.float64)))
+    # and within the SURVEY §8d bar of the oracle's (sampler rounding moves these costs by ~3e-8 relative)
+    np.testing.assert_allclose(gpu_cost, cost, rtol=1e-4)
     if res.best_index != i:  # only acceptable when the two costs tie within the parity bar
         assert abs(cost[res.best_index] - cost[i]) <= 1e-4 * abs(cost[i])
     np.testing.assert_allclose(res.u_best, u[res.best_index].numpy(), rtol=1e-4, atol=1e-4 * 20)
@@ -156,3 +165,96 @@ def test_native_step_ties_pick_lowest_index():
     c = res.costs.cpu()
     assert torch.all(c == c[0])
     assert res.best_index == 0 and res.best_cost == float(c[0])
+
+
+@pytest.mark.parametrize("native", [False, True])
+@pytest.mark.parametrize("clip_rule", ["chain", "final"])
+def test_clip_rule_cosine_250_clamped_candidates(native, clip_rule):
+    """Cosine N=250: posterior_mean_coef1[0] = 1.0000888 (fp32), so a candidate whose x0 estimate is
+    clamped at step 0 ends at +-1.0000888 - inside the 1e-4 tolerance of LimitsNormalizer's test. Under
+    the reference composition (run_CFG(return_chain=True), unnormalize_states(chain)) x_T ~ N(0, 1) is in
+    the test, the flag is set and those candidates are clipped to +-1; under the final-samples rule they
+    are not. Both rules against the oracle; the chain rule keeps every action inside its limits."""
+    d, H, C, N, B = 1, 32, 5, 250, 256
+    net = make_mlp(d, H, C, seed=4)
+    lo, hi = np.array([-3.0]), np.array([3.0])
+    plan = DiffusionMPC(NetSpec("mlp", d, H, C, dtype="f32x3"), net.state_dict(), variance_schedule="cosine",
+                        n_diffusion_steps=N, action_limits=(lo, hi))
+    red = lambda th: (th - np.pi) ** 2 / -np.pi + np.pi  # noqa: E731
+    x0 = np.array([0.3, 0.1, 0.95 * np.pi, -0.2, red(0.95 * np.pi)])
+    noise = torch.randn(N + 1, B, H, d, generator=torch.Generator().manual_seed(8))
+    res = plan.mpc_step(x0, systems.cartpole_lin5(), B, w=0.01, noise=noise, native=native, clip_rule=clip_rule)
+    from oracle import normalizer as onorm
+    ctx = onorm.normalize(torch.from_numpy(x0)[None], -torch.ones(C), torch.ones(C)).float()
+    chain = osam.ddpm_cfg(net, osch.buffers("cosine", N), ctx.expand(B, C), 0.01, B, H, noise=noise, return_chain=True)
+    lo32, hi32 = torch.from_numpy(lo.astype(np.float32)), torch.from_numpy(hi.astype(np.float32))
+    final = chain[-1]
+    assert (final.abs() > 1).any() and final.abs().max() <= 1 + 1e-4, "the case must hold clamped candidates"
+    u = onorm.unnormalize(chain if clip_rule == "chain" else final, lo32, hi32)
+    u = u[-1] if clip_rule == "chain" else u
+    cost = osys.rollout_cost("cartpole_lin5", x0, u.double().numpy())
+    np.testing.assert_allclose(res.costs.cpu().numpy(), cost, rtol=1e-4)
+    i = osys.argmin(cost)
+    assert res.best_index == i or abs(cost[res.best_index] - cost[i]) <= 1e-4 * abs(cost[i])
+    np.testing.assert_allclose(res.u_best, u[res.best_index].numpy(), rtol=1e-4, atol=1e-4 * 3)
+    if clip_rule == "chain":
+        assert np.all(res.u_best >= lo[0]) and np.all(res.u_best <= hi[0])
+
+
+def test_clip_flag_nan_semantics():
+    """torch's x.max() / x.min() are NaN when x holds a NaN, so LimitsNormalizer does NOT clip even if other
+    values are out of range; the device flag follows (code 2) and unnormalise leaves the values unclipped."""
+    plan = _planner(d=2, H=16, C=2, lo=-2.0, hi=3.0)
+    x = np.full((4, 16, 2), 0.5, np.float32)
+    x[1, 3, 0] = 1.7
+    assert int(plan.clip_flag(torch.from_numpy(x).cuda()).item()) == 1
+    x[2, 5, 1] = np.nan
+    assert int(plan.clip_flag(torch.from_numpy(x).cuda()).item()) == 2
+    got = plan.unnormalize_states(torch.from_numpy(x).cuda()).cpu()
+    from oracle import normalizer as onorm
+    ref = onorm.unnormalize(torch.from_numpy(x), torch.tensor([-2.0, -2.0]), torch.tensor([3.0, 3.0]))
+    assert torch.equal(got.isnan(), ref.isnan())
+    assert torch.equal(got[~got.isnan()], ref[~ref.isnan()])
+    assert float(got[1, 3, 0]) == float(ref[1, 3, 0]) > 3.0  # not clipped
+
+
+@pytest.mark.parametrize("kind", ["mlp_f32x3", "mlp_f32", "unet_f32x3"])
+def test_chain_absmax_matches_chain(kind):
+    """sample_trajectories(absmax_out=...) == max |x| over run_CFG's whole chain, per candidate."""
+    d, H, C, N, B = 2, 16, 4, 25, 45
+    if kind.startswith("mlp"):
+        net = make_mlp(d, H, C, seed=6)
+        spec = NetSpec("mlp", d, H, C, dtype=kind.split("_")[1])
+    else:
+        net = make_unet(d, C, seed=6)
+        spec = NetSpec("unet", d, H, C, dtype="f32x3")
+    plan = DiffusionMPC(spec, net.state_dict(), n_diffusion_steps=N)
+    ctx = torch.rand(B if kind == "mlp_f32" else 1, C) * 2 - 1
+    am = torch.empty(B, dtype=torch.float32, device="cuda")
+    chain = plan.sample_trajectories(ctx, B, H, seed=3, return_chain=True, absmax_out=am)
+    want = chain.abs().amax(dim=(0, 2, 3))
+    assert torch.equal(am, want)
+
+
+@pytest.mark.parametrize("kind", ["mlp", "unet"])
+def test_nonfinite_weights_fail_loudly(kind):
+    """SURVEY §5 failure detection: a NaN in the weights makes every sample NaN; mpc_step must return
+    MPCD_ENONFINITE (MpcdError) instead of a silently selected garbage trajectory, and a finite run reports
+    its flags (clip applied under the chain rule)."""
+    from mpc_via_diffusion_model_amd import _native as N
+    d, H, C = 1, 32, 5
+    net = make_mlp(d, H, C, seed=1) if kind == "mlp" else make_unet(d, C, seed=1)
+    sd = {k: v.clone() for k, v in net.state_dict().items()}
+    spec = NetSpec(kind, d, H, C, dtype="f32x3")
+    x0 = np.array([0.3, 0.1, 0.95 * np.pi, -0.2, 0.1])
+    ok = DiffusionMPC(spec, sd, n_diffusion_steps=25).mpc_step(x0, systems.cartpole_lin5(), 64, seed=3)
+    assert np.isfinite(ok.best_cost) and ok.flags & N.MPCD_STEP_CLIPPED  # x_T ~ N(0,1) is in the chain
+    first = next(k for k in sd if k.endswith("weight") and sd[k].dim() >= 2)
+    sd[first].view(-1)[0] = float("nan")
+    bad = DiffusionMPC(spec, sd, n_diffusion_steps=25)
+    with pytest.raises(N.MpcdError) as ei:
+        bad.mpc_step(x0, systems.cartpole_lin5(), 64, seed=3)
+    assert ei.value.status == N.MPCD_ENONFINITE
+    fl = ctypes.c_int32()
+    N.check(bad._lib.mpcd_last_step_flags(bad._ctx, ctypes.byref(fl)), "flags")
+    assert fl.value & N.MPCD_STEP_NONFINITE_WINNER and fl.value & N.MPCD_STEP_NAN_SAMPLES
