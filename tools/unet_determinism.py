@@ -1,5 +1,7 @@
-"""Diagnostics (GPU) round 3: which U-Net conv layer / tiling is nondeterministic at large B
-(MPCD_UNET_FORCE_LAYER), and the U-Net chain |x| maxima with a one-hot x_T."""
+"""Diagnostics (GPU): run-to-run determinism of every U-Net conv layer under each forced tiling at a
+batch large enough for several workgroups per CU (MPCD_UNET_FORCE_LAYER applies the forced candidate
+to one conv, the others take MPCD_UNET_FORCE_BASE), and the chain |x| maxima with a one-hot x_T.
+This is how the packed-f32 Mish issue of the mx epilogue was localised (unet_mx.hip epilogue)."""
 import os
 import sys
 
