@@ -30,6 +30,14 @@ MPCD_DEV float mish(float x)
     return x * __builtin_fmaf(-2.0f, r, 1.0f);
 }
 
+// torch.clamp(x, -1, 1) / torch.clip: a NaN stays NaN (fminf / fmaxf alone would return the bound), so a
+// non-finite noise prediction propagates to the samples as in the reference instead of turning into -1.
+MPCD_DEV float clamp1(float x)
+{
+    const float c = fminf(fmaxf(x, -1.0f), 1.0f);
+    return x != x ? x : c;
+}
+
 // The accurate reference form (expf + IEEE divide), kept for the low-volume prologue kernels.
 MPCD_DEV float mish_precise(float x)
 {

@@ -273,17 +273,17 @@ struct MlpKernel {
                         const float x0c = sp.a * xv - sp.b * ec[r];
                         const float x0u = sp.a * xv - sp.b * eu[r];
                         float x0 = p.wp1 * x0c - p.wf * x0u;
-                        x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+                        x0 = clamp1(x0);
                         const float mean = sp.c1 * x0 + sp.c2 * xv;
                         o = (sp.flags & PLAN_NOISE) ? mean + sp.std * nz[j][0][r] : mean;
                     } else if (SMODE == MODE_DDIM_CFG) {
                         float x0 = p.wp1 * (sp.a * xv - sp.b * ec[r]) - p.wf * (sp.a * xv - sp.b * eu[r]);
-                        if (p.clamp_x0) x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+                        if (p.clamp_x0) x0 = clamp1(x0);
                         const float e = p.wp1 * ec[r] - p.wf * eu[r];
                         o = (sp.flags & PLAN_FINAL) ? x0 : x0 * sp.sqan + sp.cn * e;
                     } else {  // MODE_DDIM, 3-arg net
                         float x0 = sp.a * xv - sp.b * ec[r];
-                        if (p.clamp_x0) x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+                        if (p.clamp_x0) x0 = clamp1(x0);
                         o = (sp.flags & PLAN_FINAL) ? x0 : x0 * sp.sqan + sp.cn * ec[r];
                     }
                     xn[r] = o;

@@ -194,7 +194,7 @@ __global__ __launch_bounds__(256) void clip_flag_kernel(const float *x, int64_t 
 
 __device__ __forceinline__ float unnorm1(float v, bool clip, float mn, float mx)
 {
-    if (clip) v = fminf(fmaxf(v, -1.0f), 1.0f);
+    if (clip) v = clamp1(v);
     const float h = (v + 1.0f) / 2.0f;
     return h * (mx - mn) + mn;
 }

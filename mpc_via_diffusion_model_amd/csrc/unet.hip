@@ -302,17 +302,17 @@ __global__ void update_kernel(float *x, const float *eps, int64_t batch, int fla
             const float x0c = sp.a * xr - sp.b * ec[r];
             const float x0u = sp.a * xr - sp.b * eu[r];
             float x0 = wp1 * x0c - wf * x0u;
-            x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+            x0 = clamp1(x0);
             const float mean = sp.c1 * x0 + sp.c2 * xr;
             o[r] = (sp.flags & PLAN_NOISE) ? mean + sp.std * z[r] : mean;
         } else if (mode == MODE_DDIM_CFG) {
             float x0 = wp1 * (sp.a * xr - sp.b * ec[r]) - wf * (sp.a * xr - sp.b * eu[r]);
-            if (clamp_x0) x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+            if (clamp_x0) x0 = clamp1(x0);
             const float e = wp1 * ec[r] - wf * eu[r];
             o[r] = (sp.flags & PLAN_FINAL) ? x0 : x0 * sp.sqan + sp.cn * e;
         } else {
             float x0 = sp.a * xr - sp.b * ec[r];
-            if (clamp_x0) x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+            if (clamp_x0) x0 = clamp1(x0);
             o[r] = (sp.flags & PLAN_FINAL) ? x0 : x0 * sp.sqan + sp.cn * ec[r];
         }
     }
