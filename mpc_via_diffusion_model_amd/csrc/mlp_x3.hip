@@ -620,8 +620,8 @@ struct MlpX3 {
         {
             const uint64_t t = __builtin_readcyclecounter();
             tacc[2 * 15] += t - tprev;
-            if (p.dbg && blockIdx.x < 8 && lane == 0)
-                for (int i = 0; i < 32; ++i) p.dbg[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + i] = (float)tacc[i];
+            if (p.dbg && blockIdx.x < 32 / WAVES && lane == 0)  // 32 wave slots
+                for (int i = 0; i < 32; ++i) p.dbg[(blockIdx.x * WAVES + (threadIdx.x >> 6)) * 32 + i] = (float)tacc[i];
             if (p.dbg && threadIdx.x == 0) {  // per-block loop start / end (memrealtime, low 32 bits)
                 p.dbg[4096 + blockIdx.x * 2] = __builtin_bit_cast(float, (uint32_t)rt0);
                 p.dbg[4096 + blockIdx.x * 2 + 1] = __builtin_bit_cast(float, (uint32_t)__builtin_amdgcn_s_memrealtime());

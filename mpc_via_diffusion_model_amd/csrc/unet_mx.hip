@@ -28,9 +28,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <fstream>
 #include <functional>
 #include <map>
 #include <mutex>
+#include <sstream>
 #include <tuple>
 #include <type_traits>
 #include <vector>
@@ -753,6 +755,10 @@ std::map<MxKey, MxChoice> g_mx_cache;  // measured pick per layer shape and batc
 // mpcd_unet_force_tiling: -1 = measured picks; conv >= 0: candidate (conv mod count) of every conv launch;
 // block -2 = never fuse, >= 0: fused candidate (block mod count) of every fusable block
 std::atomic<int> g_force_conv{-1}, g_force_block{-1};
+// persistent picks (MPCD_UNET_TUNE_CACHE), defined with the block cache below
+void tune_cache_load();
+void tune_cache_append(const std::string &line);
+void key_write(std::ostringstream &os, const MxKey &k);
 
 bool autotune_on()
 {
@@ -957,6 +963,7 @@ hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::
     }
     {
         std::lock_guard<std::mutex> g(g_mx_mu);
+        tune_cache_load();
         auto it = g_mx_cache.find(key);
         if (it != g_mx_cache.end()) {
             pick = it->second;
@@ -994,6 +1001,12 @@ hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::
         (void)hipGetLastError();
         std::lock_guard<std::mutex> g(g_mx_mu);
         g_mx_cache[key] = pick;
+        std::ostringstream os;
+        os << "mx ";
+        key_write(os, key);
+        os << " : " << pick.rb << ' ' << pick.t.nn << ' ' << pick.t.nc << ' ' << pick.pers << ' ' << pick.alias << ' '
+           << pick.lds << ' ' << pick.stat_off;
+        tune_cache_append(os.str());
     }
     static const int skip = [] {  // experiment knob: skip kernel phases (results are garbage)
         const char *e = getenv("MPCD_UNET_SKIP");
@@ -1023,6 +1036,67 @@ struct RtbKey {
     bool operator<(const RtbKey &o) const { return a < o.a || (!(o.a < a) && b < o.b); }
 };
 std::map<RtbKey, RtbChoice> g_rtb_cache;
+
+// MPCD_UNET_TUNE_CACHE=<file>: the measured picks persist across processes (loaded on first use, every
+// new pick appended), so a profiling run and the bench use the same tilings and a service skips the
+// autotune on start-up. One line per pick: "mx <key> : <choice>" / "rtb <key1> <key2> : <choice>".
+const char *tune_cache_path()
+{
+    static const char *p = [] {
+        const char *e = getenv("MPCD_UNET_TUNE_CACHE");
+        return e && e[0] ? e : nullptr;
+    }();
+    return p;
+}
+void key_read(std::istringstream &is, MxKey &k)
+{
+    long long r, xr;
+    is >> k.kind >> k.planes >> k.ca >> k.cb >> k.cout >> k.lin >> k.lout >> k.epi >> r >> xr;
+    k.rows = r;
+    k.x_rows = xr;
+}
+void key_write(std::ostringstream &os, const MxKey &k)
+{
+    os << k.kind << ' ' << k.planes << ' ' << k.ca << ' ' << k.cb << ' ' << k.cout << ' ' << k.lin << ' ' << k.lout << ' '
+       << k.epi << ' ' << (long long)k.rows << ' ' << (long long)k.x_rows;
+}
+void tune_cache_load()  // under g_mx_mu
+{
+    static bool done = false;
+    if (done || !tune_cache_path()) return;
+    done = true;
+    std::ifstream f(tune_cache_path());
+    std::string line;
+    while (std::getline(f, line)) {
+        std::istringstream is(line);
+        std::string tag, colon;
+        is >> tag;
+        if (tag == "mx") {
+            MxKey k{};
+            MxChoice c{};
+            key_read(is, k);
+            size_t lds;
+            is >> colon >> c.rb >> c.t.nn >> c.t.nc >> c.pers >> c.alias >> lds >> c.stat_off;
+            c.lds = lds;
+            if (is && colon == ":") g_mx_cache[k] = c;
+        } else if (tag == "rtb") {
+            RtbKey k{};
+            RtbChoice c{};
+            key_read(is, k.a);
+            key_read(is, k.b);
+            size_t lds;
+            is >> colon >> c.fused >> c.rb >> c.t.nn >> c.t.nc >> lds >> c.x_off >> c.stat_off;
+            c.lds = lds;
+            if (is && colon == ":") g_rtb_cache[k] = c;
+        }
+    }
+}
+void tune_cache_append(const std::string &line)  // under g_mx_mu
+{
+    if (!tune_cache_path()) return;
+    std::ofstream f(tune_cache_path(), std::ios::app);
+    f << line << '\n';
+}
 
 template <int P>
 hipError_t launch_fused(const ConvMK2 &k2, Tile t, size_t lds, hipStream_t st)
@@ -1129,6 +1203,7 @@ hipError_t unet_launch_mx_rtb(int planes, ConvMK &k1, ConvMK &k2, hipStream_t st
     bool have = false;
     {
         std::lock_guard<std::mutex> g(g_mx_mu);
+        tune_cache_load();
         auto it = g_rtb_cache.find(key);
         if (it != g_rtb_cache.end()) {
             pick = it->second;
@@ -1176,6 +1251,14 @@ hipError_t unet_launch_mx_rtb(int planes, ConvMK &k1, ConvMK &k2, hipStream_t st
         (void)hipGetLastError();
         std::lock_guard<std::mutex> g(g_mx_mu);
         g_rtb_cache[key] = pick;
+        std::ostringstream os;
+        os << "rtb ";
+        key_write(os, key.a);
+        os << ' ';
+        key_write(os, key.b);
+        os << " : " << pick.fused << ' ' << pick.rb << ' ' << pick.t.nn << ' ' << pick.t.nc << ' ' << pick.lds << ' '
+           << pick.x_off << ' ' << pick.stat_off;
+        tune_cache_append(os.str());
     }
     if (mode == 1 && !pick.fused) pick = cands[0];
     if (!pick.fused) return unfused();
