@@ -21,6 +21,7 @@
 // and the shared context part of every cond_mlp are pre-summed into the accumulator init per step
 // (TPC: context rows, TPU: masked rows). Per-candidate contexts use the exact-f32 kernel.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "internal.h"
@@ -29,7 +30,10 @@
 namespace {
 using namespace mlpc;
 
-constexpr int ROWS = 32;
+// Rows per workgroup: 32 (16 candidates x {context, masked} for CFG) or, for batches too small to give
+// every CU a workgroup, 16 (8 candidates x 2): one 16-column MFMA tile per layer, half the MFMAs per
+// wave and per step, twice the workgroups (mlp_x3_rows() picks; MPCD_MLP_ROWS=16|32 forces).
+constexpr int ROWS_MAX = 32;
 // WAVES = 8 (two per SIMD): while one wave of a SIMD waits on a barrier, an LDS read or its own
 // MFMA chain, the other issues, and a bf16 MFMA leaves vector issue free for 8 of its 16 cycles, so
 // one wave's Mish / split VALU runs under the other's MFMAs. Hidden layers then map as PAIR8
@@ -73,7 +77,7 @@ MPCD_DEV void split3(const f32x4 &v, u32x2 &p0, u32x2 &p1, u32x2 &p2)
 // ---- LDS layout (bytes). Activation buffers hold three bf16 planes of ROWS rows; a row stride of
 // 16 mod 256 bytes keeps the 16-lane groups of a ds_read_b128 conflict-free (MI355X_MICROARCH LDS
 // table: lane (q, col) reads 16 B at row col, chunk q).
-template <int D0, int NB>
+template <int D0, int NB, int ROWS>
 struct Lds3 {
     static constexpr int CPW = ROWS / NB;  // candidates per workgroup
     static constexpr int RS = 272;         // row stride, widths <= 128
@@ -109,8 +113,8 @@ struct Lds3 {
     static constexpr int out_pl(int l) { return (l == 5 || l == 7) ? PL2 : PL; }
 };
 
-template <int N>
-constexpr int mode_for() { return WAVES == 8 ? (N >= 128 ? PAIR8 : WIDE8) : N == 32 ? SPLIT : PAIRED; }
+template <int N, int R = 32>
+constexpr int mode_for() { return WAVES == 8 ? ((N >= 128 || R == 16) ? PAIR8 : WIDE8) : N == 32 ? SPLIT : PAIRED; }
 
 constexpr int epi_of(int l) { return l == 12 ? EPI_NONE : (l % 2 == 1) ? EPI_CMISH : EPI_MISH; }
 
@@ -180,12 +184,16 @@ MPCD_DEV void load_x3(u32x4 (&x)[3], const char *base, int plane_stride)
     for (int pl = 0; pl < 3; ++pl) x[pl] = *reinterpret_cast<const u32x4 *>(base + pl * plane_stride);
 }
 
-template <int D0, int SMODE, bool CTX>
+template <int D0, int SMODE, bool CTX, int R>
 struct MlpX3 {
     static constexpr int NB = (SMODE == MODE_DDIM || SMODE == MODE_EPS1) ? 1 : 2;
     static constexpr bool IS_DDPM = SMODE == MODE_DDPM_CFG || SMODE == MODE_DDPM_XN;
+    static_assert(R == 32 || (R == 16 && WAVES == 8), "16-row workgroups need the 8-wave layout");
     using A = Arch<D0>;
-    using L = Lds3<D0, NB>;
+    using L = Lds3<D0, NB, R>;
+    // R = 16 with CFG: columns 0-7 are the context rows of candidates 0-7, 8-15 their masked rows
+    static MPCD_DEV int cand_of(int ct, int col) { return NB == 2 ? (R == 16 ? (col & 7) : col) : ct * 16 + col; }
+    static MPCD_DEV bool masked_of(int ct, int col) { return NB == 2 && (R == 16 ? col >= 8 : ct == 1); }
     static constexpr int CPW = L::CPW;
     static constexpr int QUADS = D0 / 4;
     using FW = WFrag3<32, D0, PAIRED>;
@@ -281,12 +289,12 @@ struct MlpX3 {
     // ahead rather than all up front (the partner wave covers the LDS latency), which keeps the
     // register budget of two waves per SIMD.
     template <int l>
-    static MPCD_DEV void hidden8(const WFrag3<A::K[l], A::N[l], mode_for<A::N[l]>()> &f, char *lds, int wave, int lane)
+    static MPCD_DEV void hidden8(const WFrag3<A::K[l], A::N[l], mode_for<A::N[l], R>()> &f, char *lds, int wave, int lane)
     {
-        constexpr int K = A::K[l], N = A::N[l], MODE = mode_for<N>(), EPI = epi_of(l);
+        constexpr int K = A::K[l], N = A::N[l], MODE = mode_for<N, R>(), EPI = epi_of(l);
         using F = WFrag3<K, N, MODE>;
         constexpr int T = F::T, KC = F::KC, NT = N / 16;
-        constexpr int NCT = MODE == PAIR8 ? 2 : 1;
+        constexpr int NCT = MODE == PAIR8 ? R / 16 : 1;
         static_assert(MODE == PAIR8 || MODE == WIDE8, "8-wave layer modes");
         const int col = lane & 15, q = lane >> 4;
         const bool in_shared = l == 0 && NB == 2;  // CFG: both branches read the candidate's x
@@ -299,7 +307,7 @@ struct MlpX3 {
         for (int c = 0; c < NCT; ++c) {
             const int ct = ct_of(c);
             const float *init = reinterpret_cast<const float *>(
-                lds + (EPI == EPI_CMISH ? ((NB == 2 && ct == 1) ? L::TPU : L::TPC) + cond_off(l / 2) * 4
+                lds + (EPI == EPI_CMISH ? (masked_of(ct, col) ? L::TPU : L::TPC) + cond_off(l / 2) * 4
                                         : L::BI + A::boff(l) * 4));
 #pragma unroll
             for (int j = 0; j < T; ++j)
@@ -308,7 +316,7 @@ struct MlpX3 {
         auto ldx = [&](u32x4 (&x)[NCT][3], int kc) {
 #pragma unroll
             for (int c = 0; c < NCT; ++c) {
-                const int row = in_shared ? col : ct_of(c) * 16 + col;
+                const int row = in_shared ? cand_of(ct_of(c), col) : ct_of(c) * 16 + col;
                 load_x3(x[c], lds + L::in_off(l) + row * L::in_rs(l) + (kc * 32 + 8 * q) * 2, L::in_pl(l));
             }
         };
@@ -352,7 +360,7 @@ struct MlpX3 {
     }
 
     template <int l>
-    static MPCD_DEV void layer(const WFrag3<A::K[l], A::N[l], mode_for<A::N[l]>()> &f, char *lds, int wave, int lane)
+    static MPCD_DEV void layer(const WFrag3<A::K[l], A::N[l], mode_for<A::N[l], R>()> &f, char *lds, int wave, int lane)
     {
         if constexpr (WAVES == 8) hidden8<l>(f, lds, wave, lane);
         else hidden<l>(f, lds, wave, lane);
@@ -378,6 +386,7 @@ struct MlpX3 {
         constexpr int T = FW::T, NT = D0 / 16;
         const int col = lane & 15, q = lane >> 4;
         const float *bias = reinterpret_cast<const float *>(lds + L::BI + A::boff(13) * 4);
+        constexpr int NCT = R / 16;  // column tiles
         f32x4 acc[T][2];
 #pragma unroll
         for (int j = 0; j < T; ++j) {  // idle tiles (D0 = 32, waves 2-3) read n-tile 0, unused
@@ -385,12 +394,27 @@ struct MlpX3 {
             acc[j][0] = acc[j][1] = *reinterpret_cast<const f32x4 *>(bias + nt * 16 + 4 * q);
         }
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
+        for (int c = 0; c < NCT; ++c) {
             u32x4 x[3];
             load_x3(x, lds + L::T1 + (c * 16 + col) * L::RS + 8 * q * 2, L::PL);
 #pragma unroll
             for (int j = 0; j < T; ++j)
                 if (NT % 4 == 0 || wave + 4 * j < NT) acc[j][c] = mfma_x3(f.v[j][0], x, acc[j][c]);
+        }
+        if (R == 16 && NB == 2) {
+            // column c holds candidate c & 7's context row (c < 8) or masked row (c >= 8): bring the masked
+            // row's eps next to the context row's (DPP row_ror:8 swaps the two halves of each 16-lane row)
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    // element to a scalar first: clang lowers __builtin_bit_cast of an ext-vector element
+                    // lvalue as a read of element 0
+                    const float e = acc[j][0][r];
+                    acc[j][1][r] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                        0, __builtin_bit_cast(int, e), 0x128, 0xF, 0xF, false));
+                }
+            if (col >= 8) return;  // lanes of the masked rows: their eps went to lane col - 8
         }
         const bool last = s == p.n_steps - 1;
 #pragma unroll
@@ -399,8 +423,8 @@ struct MlpX3 {
             if (NT % 4 != 0 && nt >= NT) continue;
             const int n = nt * 16 + 4 * q;
 #pragma unroll
-            for (int g = 0; g < (NB == 2 ? 1 : 2); ++g) {
-                // NB == 2: one candidate per lane column, eps_c = tile 0, eps_u = tile 1
+            for (int g = 0; g < (NB == 2 ? 1 : NCT); ++g) {
+                // NB == 2: one candidate per lane column, eps_c = tile 0, eps_u = tile 1 (R = 16: the DPP swap)
                 // NB == 1: column tile g holds candidates 16g..16g+15
                 const int cl = NB == 2 ? col : g * 16 + col;
                 const f32x4 ec = acc[j][NB == 2 ? 0 : g];
@@ -465,8 +489,8 @@ struct MlpX3 {
             const int nt = wave + 4 * j;
             if (NT % 4 != 0 && nt >= NT) continue;
             const int n = nt * 16 + 4 * q;
-            const int64_t gc = cand0 + col;  // DDPM-CFG: NB == 2, one candidate per column
-            if (gc >= p.batch) continue;
+            const int64_t gc = cand0 + col;  // DDPM-CFG: NB == 2, one candidate per column (R = 16: columns < 8)
+            if (gc >= p.batch || (R == 16 && col >= 8)) continue;
             if (SMODE == MODE_DDPM_XN)
                 nz[j][0] = *reinterpret_cast<const f32x4 *>(p.noise + ((size_t)(s + 1) * p.batch + gc) * D0 + n);
             else
@@ -510,7 +534,7 @@ struct MlpX3 {
             store_x(lds, c, qd * 4, z);
         }
 
-        WFrag3<A::K[0], A::N[0], mode_for<A::N[0]>()> w0;
+        WFrag3<A::K[0], A::N[0], mode_for<A::N[0], R>()> w0;
         load_w3(w0, W(0), wave, lane16);
         f32x4 nz[NZT][NB];
         StepPlan sp = load_plan(p.plan, 0);
@@ -537,7 +561,7 @@ struct MlpX3 {
         for (int s = 0; s < p.n_steps; ++s) {
             // launder the weight base: stops LICM hoisting every layer's weight loads out of the loop
             asm volatile("" : "+s"(wofs), "+v"(lane16));
-            WFrag3<A::K[1], A::N[1], mode_for<A::N[1]>()> w1;
+            WFrag3<A::K[1], A::N[1], mode_for<A::N[1], R>()> w1;
             load_w3(w1, W(1), wave, lane16);
             bar(0);
             // this step's time projections + cond biases (+ shared context part) -> TPU / TPC
@@ -548,47 +572,47 @@ struct MlpX3 {
             }
             tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 1 < p.n_steps ? s + 1 : s) * COND_TOTAL)[tpi];
             layer<0>(w0, lds, wave, lane);
-            WFrag3<A::K[2], A::N[2], mode_for<A::N[2]>()> w2;
+            WFrag3<A::K[2], A::N[2], mode_for<A::N[2], R>()> w2;
             load_w3(w2, W(2), wave, lane16);
             bar(1);
             layer<1>(w1, lds, wave, lane);
-            WFrag3<A::K[3], A::N[3], mode_for<A::N[3]>()> w3;
+            WFrag3<A::K[3], A::N[3], mode_for<A::N[3], R>()> w3;
             load_w3(w3, W(3), wave, lane16);
             bar(2);
             layer<2>(w2, lds, wave, lane);
-            WFrag3<A::K[4], A::N[4], mode_for<A::N[4]>()> w4;
+            WFrag3<A::K[4], A::N[4], mode_for<A::N[4], R>()> w4;
             load_w3(w4, W(4), wave, lane16);
             bar(3);
             layer<3>(w3, lds, wave, lane);
-            WFrag3<A::K[5], A::N[5], mode_for<A::N[5]>()> w5;
+            WFrag3<A::K[5], A::N[5], mode_for<A::N[5], R>()> w5;
             load_w3(w5, W(5), wave, lane16);
             bar(4);
             layer<4>(w4, lds, wave, lane);
-            WFrag3<A::K[6], A::N[6], mode_for<A::N[6]>()> w6;
+            WFrag3<A::K[6], A::N[6], mode_for<A::N[6], R>()> w6;
             load_w3(w6, W(6), wave, lane16);
             bar(5);
             layer<5>(w5, lds, wave, lane);
-            WFrag3<A::K[7], A::N[7], mode_for<A::N[7]>()> w7;
+            WFrag3<A::K[7], A::N[7], mode_for<A::N[7], R>()> w7;
             load_w3(w7, W(7), wave, lane16);
             bar(6);
             layer<6>(w6, lds, wave, lane);
-            WFrag3<A::K[8], A::N[8], mode_for<A::N[8]>()> w8;
+            WFrag3<A::K[8], A::N[8], mode_for<A::N[8], R>()> w8;
             load_w3(w8, W(8), wave, lane16);
             bar(7);
             layer<7>(w7, lds, wave, lane);
-            WFrag3<A::K[9], A::N[9], mode_for<A::N[9]>()> w9;
+            WFrag3<A::K[9], A::N[9], mode_for<A::N[9], R>()> w9;
             load_w3(w9, W(9), wave, lane16);
             bar(8);
             layer<8>(w8, lds, wave, lane);
-            WFrag3<A::K[10], A::N[10], mode_for<A::N[10]>()> w10;
+            WFrag3<A::K[10], A::N[10], mode_for<A::N[10], R>()> w10;
             load_w3(w10, W(10), wave, lane16);
             bar(9);
             layer<9>(w9, lds, wave, lane);
-            WFrag3<A::K[11], A::N[11], mode_for<A::N[11]>()> w11;
+            WFrag3<A::K[11], A::N[11], mode_for<A::N[11], R>()> w11;
             load_w3(w11, W(11), wave, lane16);
             bar(10);
             layer<10>(w10, lds, wave, lane);
-            WFrag3<A::K[12], A::N[12], mode_for<A::N[12]>()> w12;
+            WFrag3<A::K[12], A::N[12], mode_for<A::N[12], R>()> w12;
             load_w3(w12, W(12), wave, lane16);
             bar(11);
             layer<11>(w11, lds, wave, lane);
@@ -613,8 +637,9 @@ struct MlpX3 {
         }
         if (SMODE != MODE_EPS && SMODE != MODE_EPS1 && p.chain_absmax) {
             const int col = lane & 15;
-            store_chain_absmax<CPW, THREADS>(reinterpret_cast<uint32_t *>(lds + L::AMX), am, NB == 2 ? col : col,
-                                             NB == 2 ? -1 : 16 + col, wave < 4, p.chain_absmax, cand0, p.batch);
+            store_chain_absmax<CPW, THREADS>(reinterpret_cast<uint32_t *>(lds + L::AMX), am, col,
+                                             (NB == 2 || R == 16) ? -1 : 16 + col,
+                                             wave < 4 && (NB == 1 || R == 32 || col < 8), p.chain_absmax, cand0, p.batch);
         }
 #ifdef MPCD_PROF_LAYERS
         {
@@ -635,27 +660,54 @@ struct MlpX3 {
     }
 };
 
-template <int D0, int SMODE, bool CTX>
+template <int D0, int SMODE, bool CTX, int R>
 __global__ __launch_bounds__(THREADS, 1) void mlp_x3_kernel(const MlpSampleArgs p)
 {
-    MlpX3<D0, SMODE, CTX>::run(p);
+    MlpX3<D0, SMODE, CTX, R>::run(p);
 }
 
-template <int D0, int SMODE, bool CTX>
-hipError_t launch_x3(const MlpSampleArgs &a, hipStream_t stream)
+template <int D0, int SMODE, bool CTX, int R>
+hipError_t launch_x3_r(const MlpSampleArgs &a, hipStream_t stream)
 {
-    using L = Lds3<D0, MlpX3<D0, SMODE, CTX>::NB>;
+    using L = Lds3<D0, MlpX3<D0, SMODE, CTX, R>::NB, R>;
     static_assert(L::total <= 160 * 1024, "LDS budget (160 KiB per CU)");
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&mlp_x3_kernel<D0, SMODE, CTX>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&mlp_x3_kernel<D0, SMODE, CTX, R>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     const int64_t blocks = (a.batch + L::CPW - 1) / L::CPW;
-    hipLaunchKernelGGL((mlp_x3_kernel<D0, SMODE, CTX>), dim3((unsigned)blocks), dim3(THREADS), (size_t)L::total, stream, a);
+    hipLaunchKernelGGL((mlp_x3_kernel<D0, SMODE, CTX, R>), dim3((unsigned)blocks), dim3(THREADS), (size_t)L::total, stream,
+                       a);
     return hipGetLastError();
+}
+
+// 16-row workgroups when 32-row ones would leave CUs idle (fewer than one per CU)
+int mlp_x3_rows(int64_t batch, int nb)
+{
+    static const int forced = [] {
+        const char *e = getenv("MPCD_MLP_ROWS");
+        return e && e[0] ? atoi(e) : 0;
+    }();
+    if (forced == 16 || forced == 32) return forced;
+    static int n_cu = 0;
+    if (!n_cu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            n_cu = 256;
+    }
+    return (batch * nb + 31) / 32 < n_cu ? 16 : 32;
+}
+
+template <int D0, int SMODE, bool CTX>
+hipError_t launch_x3(const MlpSampleArgs &a, hipStream_t stream)
+{
+    constexpr int NB = MlpX3<D0, SMODE, CTX, 32>::NB;
+    return mlp_x3_rows(a.batch, NB) == 16 ? launch_x3_r<D0, SMODE, CTX, 16>(a, stream)
+                                          : launch_x3_r<D0, SMODE, CTX, 32>(a, stream);
 }
 
 template <int D0>

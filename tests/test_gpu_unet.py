@@ -207,3 +207,46 @@ def test_fused_block_bit_identical(d, H, C, B, dtype, monkeypatch):
     full = plan.sample_trajectories(ctx[:1], 40, H, seed=5)
     monkeypatch.setenv("MPCD_UNET_FUSE", "0")
     assert torch.equal(full, plan.sample_trajectories(ctx[:1], 40, H, seed=5))
+
+
+PANDA = os.path.join(HERE, "golden", "panda_test6_117600_ema.safetensors")
+
+
+def _panda_oracle_net(sd):
+    from oracle import nets
+    net = nets.ConditionedTemporalUnet(state_dim=7, context_dim=20).eval()
+    net.load_state_dict({k[6:]: v for k, v in sd.items() if k.startswith("model.")}, strict=True)
+    return net
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f32x3", "f16"])
+@pytest.mark.parametrize("B", [1, 48])
+def test_panda_trained_checkpoint_through_gpu(dtype, B):
+    """the trained panda_test6_117600 EMA net (d=7 joint torques, C=20, H=128, N=25, the
+    checkpoint's own schedule buffers) sampled as inference_diffusion_panda.py:444-449 calls it -
+    run_CFG(context, None, 0.01, n_samples, horizon=128, return_chain=True, ddpm_cart_pole_sample_fn,
+    n_diffusion_steps_without_noise=5) - with the torch.manual_seed(0) noise stream injected, against the
+    oracle chain: fp32 numerics at the 1e-4 bar, fp16 operands reported (5e-2 trajectory bound)."""
+    from safetensors.torch import load_file
+    from oracle import schedule as osch_
+    sd = load_file(PANDA)
+    plan = DiffusionMPC.from_state_dict(sd, NetSpec("unet", state_dim=7, horizon=128, context_dim=20, dtype=dtype))
+    net = _panda_oracle_net(sd)
+    bufs = {k: sd[k] for k in osch_.BUFFER_NAMES}
+    torch.manual_seed(0)
+    ctx = torch.rand(1, 20) * 2 - 1
+    noise = torch.stack([torch.randn(B, 128, 7) for _ in range(31)])  # x_T + 25 + 5 randn_like draws
+    chain = plan.run_CFG(ctx, None, 0.01, n_samples=B, horizon=128, return_chain=True, noise=noise,
+                         n_diffusion_steps_without_noise=5)
+    # the trained net amplifies fp32 rounding along its 30-step chain: the oracle's own elementwise spread when its
+    # Linear/Conv round from fp64 is 9.4e-4 at B=48, so that spread (x4) is the elementwise bar; trajectories 1e-4
+    ref, spread = oracle_sensitivity(lambda: osam.ddpm_cfg(net, bufs, ctx.expand(B, 20), 0.01, B, 128, n_wo_noise=5,
+                                                           noise=noise, return_chain=True))
+    assert tuple(chain.shape) == (31, B, 128, 7)
+    if dtype == "f16":
+        got = chain[-1].cpu()
+        rel = float(((got - ref[-1]).flatten(1).norm(dim=1) / ref[-1].flatten(1).norm(dim=1)).max())
+        print(f"panda f16 trajectory rel err {rel:.3e}")
+        assert torch.isfinite(got).all() and rel <= 5e-2
+    else:
+        assert_traj_close(chain, ref, abs_elem=max(1e-4, 4 * spread), what=f"panda {dtype} B={B}")

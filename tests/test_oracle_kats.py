@@ -142,3 +142,24 @@ def test_kat6_zoh_matrices():
     A_d, B_d = systems.ZOH_A, systems.ZOH_B
     want = [A_d[i][0] * x[0] + A_d[i][1] * x[1] + A_d[i][2] * x[2] + A_d[i][3] * x[3] + B_d[i] * 0.7 for i in range(4)]
     np.testing.assert_array_equal(osys.step("cartpole_zoh4", x, [0.7]), want)
+
+
+PANDA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "panda_test6_117600_ema.safetensors")
+
+
+def test_panda_fixture_loads_into_the_oracle():
+    """The converted panda_test6_117600 EMA fixture is a ConditionedTemporalUnet(d=7, C=20) state dict
+    (1,015,719 parameters) plus the 12 schedule buffers of N=25 exponential, equal to a recomputation."""
+    from safetensors.torch import load_file
+    sd = load_file(PANDA)
+    net = nets.ConditionedTemporalUnet(state_dim=7, context_dim=20).eval()
+    net.load_state_dict({k[6:]: v for k, v in sd.items() if k.startswith("model.")}, strict=True)
+    assert nets.param_count(net) == 1015719
+    assert torch.equal(sd["betas"], schedule.buffers("exponential", 25)["betas"])
+    import yaml
+    from mpc_via_diffusion_model_amd import formats
+    with open(PANDA.replace("_ema.safetensors", "_args.yaml")) as f:
+        args = yaml.safe_load(f)  # the checkpoint's own args.yaml (tests/golden copy)
+    assert (args["n_diffusion_steps"], args["variance_schedule"], args["use_ema"]) == (25, "exponential", True)
+    spec = formats.infer_spec(sd, args, horizon=128)
+    assert (spec.kind, spec.state_dim, spec.context_dim, spec.horizon, spec.dim_mults) == ("unet", 7, 20, 128, (1, 2, 4))
