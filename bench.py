@@ -52,7 +52,11 @@ WORKLOADS = {
 PEAK_FP32 = 157.3e12      # MI355X dense fp32 MFMA / vector peak, FLOP/s (MI355X_MICROARCH.md)
 PEAK_BF16 = 2516.6e12     # MI355X dense bf16 / fp16 MFMA peak: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz
 PMC_FILES = {("cfg2", "f32"): os.path.join(ROOT, "profiles", "r1_pmc_mlp_sampler.json"),
-             ("cfg2", "f32x3"): os.path.join(ROOT, "profiles", "r1_pmc_mlp_x3.json")}
+             ("cfg2", "f32x3"): os.path.join(ROOT, "profiles", "r1_pmc_mlp_x3.json"),
+             # U-Net: HBM bytes of one noise-net forward (every conv launch, PMC FETCH_SIZE x2 + WRITE_SIZE) at B
+             ("cfg3", "f32x3"): os.path.join(ROOT, "profiles", "r2_unet_roofline_cfg3.json"),
+             ("cfg4", "f32x3"): os.path.join(ROOT, "profiles", "r2_unet_roofline_cfg4.json"),
+             ("cfg5", "f16"): os.path.join(ROOT, "profiles", "r2_unet_roofline_cfg5.json")}
 
 
 def _rank_env():
@@ -274,7 +278,11 @@ def main():
         pmc = PMC_FILES.get((args.workload, dtype))
         if pmc and os.path.exists(pmc):
             with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                pm = json.load(f)
+            if "hbm_bytes_per_forward" in pm:  # one sample call = n_evals forwards; bytes scale with the rows
+                traffic = pm["hbm_bytes_per_forward"] * n_evals * b_local / pm["B"]
+            else:
+                traffic = pm.get("hbm_bytes_per_launch")
         gemm = {"f32": "exact fp32 MFMA (v_mfma_f32_16x16x4_f32)",
                 "f32x3": "fp32-accurate split-bf16 MFMA (3 bf16 terms per operand, 6 partial products, fp32 accumulate)",
                 "f16": "fp16 operands, fp32 accumulate (v_mfma_f32_16x16x32_f16)"}[dtype]

@@ -32,7 +32,7 @@ using namespace mlpc;
 
 // Rows per workgroup: 32 (16 candidates x {context, masked} for CFG) or, for batches too small to give
 // every CU a workgroup, 16 (8 candidates x 2): one 16-column MFMA tile per layer, half the MFMAs per
-// wave and per step, twice the workgroups (mlp_x3_rows() picks; MPCD_MLP_ROWS=16|32 forces).
+// wave and per step, twice the workgroups (mlp_x3_layout() picks).
 constexpr int ROWS_MAX = 32;
 // WAVES = 8 (two per SIMD): while one wave of a SIMD waits on a barrier, an LDS read or its own
 // MFMA chain, the other issues, and a bf16 MFMA leaves vector issue free for 8 of its 16 cycles, so
@@ -42,6 +42,14 @@ constexpr int ROWS_MAX = 32;
 // in the PAIRED form. WAVES = 4 keeps the one-wave-per-SIMD schedule (hidden()).
 #ifndef MPCD_X3_WAVES
 #define MPCD_X3_WAVES 8
+#endif
+// MPCD_X3_ILV = 1: the N = 128 layers overlap one column tile's epilogue with the other's MFMAs
+// MPCD_X3_PAIR_MIN: narrowest layer mapped PAIR8 at 32 rows (each weight fragment loaded by one wave)
+#ifndef MPCD_X3_PAIR_MIN
+#define MPCD_X3_PAIR_MIN 128
+#endif
+#ifndef MPCD_X3_ILV
+#define MPCD_X3_ILV 1
 #endif
 constexpr int THREADS = 64 * MPCD_X3_WAVES;
 constexpr int WAVES = THREADS / 64;
@@ -113,8 +121,12 @@ struct Lds3 {
     static constexpr int out_pl(int l) { return (l == 5 || l == 7) ? PL2 : PL; }
 };
 
-template <int N, int R = 32>
-constexpr int mode_for() { return WAVES == 8 ? ((N >= 128 || R == 16) ? PAIR8 : WIDE8) : N == 32 ? SPLIT : PAIRED; }
+// W = 4 with R = 16 (two workgroups per CU, see mlp_x3_layout): every layer PAIRED (wave w -> n-tiles w + 4j)
+template <int N, int R = 32, int W = WAVES>
+constexpr int mode_for()
+{
+    return W == 8 ? ((N >= MPCD_X3_PAIR_MIN || R == 16) ? PAIR8 : WIDE8) : R == 16 ? PAIRED : N == 32 ? SPLIT : PAIRED;
+}
 
 constexpr int epi_of(int l) { return l == 12 ? EPI_NONE : (l % 2 == 1) ? EPI_CMISH : EPI_MISH; }
 
@@ -184,11 +196,14 @@ MPCD_DEV void load_x3(u32x4 (&x)[3], const char *base, int plane_stride)
     for (int pl = 0; pl < 3; ++pl) x[pl] = *reinterpret_cast<const u32x4 *>(base + pl * plane_stride);
 }
 
-template <int D0, int SMODE, bool CTX, int R>
+template <int D0, int SMODE, bool CTX, int R, int W = WAVES>
 struct MlpX3 {
+    static constexpr int NTHR = 64 * W;  // threads per workgroup
     static constexpr int NB = (SMODE == MODE_DDIM || SMODE == MODE_EPS1) ? 1 : 2;
     static constexpr bool IS_DDPM = SMODE == MODE_DDPM_CFG || SMODE == MODE_DDPM_XN;
-    static_assert(R == 32 || (R == 16 && WAVES == 8), "16-row workgroups need the 8-wave layout");
+    static_assert(R == 32 || R == 16, "32 or 16 rows per workgroup");
+    static_assert(W == 8 || W == 4, "4 or 8 waves per workgroup");
+    static constexpr bool H8 = W == 8 || R == 16;  // hidden8() for every layer (else the 4-wave hidden())
     using A = Arch<D0>;
     using L = Lds3<D0, NB, R>;
     // R = 16 with CFG: columns 0-7 are the context rows of candidates 0-7, 8-15 their masked rows
@@ -203,9 +218,9 @@ struct MlpX3 {
     // (N >= 64): wave w -> n-tiles w + 4j for both column tiles (each weight fragment feeds two
     // MFMA chains). Accumulators start from the bias, or for cond layers from TPC / TPU.
     template <int l>
-    static MPCD_DEV void hidden(const WFrag3<A::K[l], A::N[l], mode_for<A::N[l]>()> &f, char *lds, int wave, int lane)
+    static MPCD_DEV void hidden(const WFrag3<A::K[l], A::N[l], mode_for<A::N[l], R, W>()> &f, char *lds, int wave, int lane)
     {
-        constexpr int K = A::K[l], N = A::N[l], MODE = mode_for<N>(), EPI = epi_of(l);
+        constexpr int K = A::K[l], N = A::N[l], MODE = mode_for<N, R, W>(), EPI = epi_of(l);
         using F = WFrag3<K, N, MODE>;
         constexpr int T = F::T, KC = F::KC;
         constexpr int NCT = MODE == SPLIT ? 1 : 2;
@@ -289,16 +304,17 @@ struct MlpX3 {
     // ahead rather than all up front (the partner wave covers the LDS latency), which keeps the
     // register budget of two waves per SIMD.
     template <int l>
-    static MPCD_DEV void hidden8(const WFrag3<A::K[l], A::N[l], mode_for<A::N[l], R>()> &f, char *lds, int wave, int lane)
+    static MPCD_DEV void hidden8(const WFrag3<A::K[l], A::N[l], mode_for<A::N[l], R, W>()> &f, char *lds, int wave, int lane)
     {
-        constexpr int K = A::K[l], N = A::N[l], MODE = mode_for<N, R>(), EPI = epi_of(l);
+        constexpr int K = A::K[l], N = A::N[l], MODE = mode_for<N, R, W>(), EPI = epi_of(l);
         using F = WFrag3<K, N, MODE>;
         constexpr int T = F::T, KC = F::KC, NT = N / 16;
-        constexpr int NCT = MODE == PAIR8 ? R / 16 : 1;
-        static_assert(MODE == PAIR8 || MODE == WIDE8, "8-wave layer modes");
+        constexpr bool PR = MODE == PAIR8 || MODE == PAIRED;  // every column tile in each wave
+        constexpr int NCT = PR ? R / 16 : 1;
+        static_assert(PR || MODE == WIDE8, "8-wave layer modes, or PAIRED on 4 waves");
         const int col = lane & 15, q = lane >> 4;
         const bool in_shared = l == 0 && NB == 2;  // CFG: both branches read the candidate's x
-        auto ct_of = [&](int c) { return MODE == PAIR8 ? c : (wave >> 2); };
+        auto ct_of = [&](int c) { return PR ? c : (wave >> 2); };
         bool ok[T];
 #pragma unroll
         for (int j = 0; j < T; ++j) ok[j] = ntile_of<K, N, MODE>(wave, j) < NT;
@@ -313,6 +329,54 @@ struct MlpX3 {
             for (int j = 0; j < T; ++j)
                 acc[j][c] = *reinterpret_cast<const f32x4 *>(init + min(ntile_of<K, N, MODE>(wave, j), NT - 1) * 16 + 4 * q);
         }
+        auto epi_tile = [&](int j, int c) {
+            const int n = ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q;
+            f32x4 v = acc[j][c];
+            if (EPI != EPI_NONE) {
+                v.x = mish(v.x);
+                v.y = mish(v.y);
+                v.z = mish(v.z);
+                v.w = mish(v.w);
+            }
+            u32x2 p0, p1, p2;
+            split3(v, p0, p1, p2);
+            char *o = lds + L::out_off(l) + (ct_of(c) * 16 + col) * L::out_rs(l) + n * 2;
+            *reinterpret_cast<u32x2 *>(o) = p0;
+            *reinterpret_cast<u32x2 *>(o + L::out_pl(l)) = p1;
+            *reinterpret_cast<u32x2 *>(o + 2 * L::out_pl(l)) = p2;
+        };
+#if MPCD_X3_ILV
+        if constexpr (PR && NCT == 2 && T == 1 && !(l == 0 && NB == 2)) {
+            // One n-tile, two column tiles (the N = 128 layers at 32 rows): column tile 0's chain first,
+            // then column tile 1's MFMAs with column tile 0's Mish / split / LDS stores scheduled in their
+            // shadow (a bf16 MFMA leaves vector issue free for 8 of its 16 cycles), 3 VALU per MFMA.
+            // Each weight fragment still feeds both column tiles from registers.
+            auto ldx1 = [&](u32x4 (&x)[3], int c, int kc) {
+                load_x3(x, lds + L::in_off(l) + (c * 16 + col) * L::in_rs(l) + (kc * 32 + 8 * q) * 2, L::in_pl(l));
+            };
+            auto chain = [&](int c) {
+                u32x4 xa[3], xb[3];
+                ldx1(xa, c, 0);
+#pragma unroll
+                for (int kc = 0; kc < KC; ++kc) {
+                    if (kc + 1 < KC) ldx1((kc & 1) ? xa : xb, c, kc + 1);
+                    acc[0][c] = mfma_x3(f.v[0][kc], (kc & 1) ? xb : xa, acc[0][c]);
+                }
+            };
+            chain(0);
+            __builtin_amdgcn_sched_barrier(0);
+            chain(1);
+            epi_tile(0, 0);
+#pragma unroll
+            for (int i = 0; i < KC * 6; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // 3 VALU
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            epi_tile(0, 1);
+            return;
+        }
+#endif
         auto ldx = [&](u32x4 (&x)[NCT][3], int kc) {
 #pragma unroll
             for (int c = 0; c < NCT; ++c) {
@@ -339,30 +403,15 @@ struct MlpX3 {
 #pragma unroll
         for (int j = 0; j < T; ++j) {
             if (!ok[j]) continue;
-            const int n = ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q;
 #pragma unroll
-            for (int c = 0; c < NCT; ++c) {
-                f32x4 v = acc[j][c];
-                if (EPI != EPI_NONE) {
-                    v.x = mish(v.x);
-                    v.y = mish(v.y);
-                    v.z = mish(v.z);
-                    v.w = mish(v.w);
-                }
-                u32x2 p0, p1, p2;
-                split3(v, p0, p1, p2);
-                char *o = lds + L::out_off(l) + (ct_of(c) * 16 + col) * L::out_rs(l) + n * 2;
-                *reinterpret_cast<u32x2 *>(o) = p0;
-                *reinterpret_cast<u32x2 *>(o + L::out_pl(l)) = p1;
-                *reinterpret_cast<u32x2 *>(o + 2 * L::out_pl(l)) = p2;
-            }
+            for (int c = 0; c < NCT; ++c) epi_tile(j, c);
         }
     }
 
     template <int l>
-    static MPCD_DEV void layer(const WFrag3<A::K[l], A::N[l], mode_for<A::N[l], R>()> &f, char *lds, int wave, int lane)
+    static MPCD_DEV void layer(const WFrag3<A::K[l], A::N[l], mode_for<A::N[l], R, W>()> &f, char *lds, int wave, int lane)
     {
-        if constexpr (WAVES == 8) hidden8<l>(f, lds, wave, lane);
+        if constexpr (H8) hidden8<l>(f, lds, wave, lane);
         else hidden<l>(f, lds, wave, lane);
     }
 
@@ -508,21 +557,21 @@ struct MlpX3 {
         int lane16 = lane * 16;
         const float *wp = p.wpack;
         int wofs = 0;
-        auto W = [&](int l) { return wp + wofs + A::woff3(l); };
+        auto wptr = [&](int l) { return wp + wofs + A::woff3(l); };
         float *bi = reinterpret_cast<float *>(lds + L::BI);
         float *bic = reinterpret_cast<float *>(lds + L::BIC);
         float *cps = reinterpret_cast<float *>(lds + L::CPS);
 
         for (int l = 0; l < NLAYER; ++l)
-            for (int i = threadIdx.x; i < A::N[l]; i += THREADS) bi[A::boff(l) + i] = wp[A::woff3(l) + 3 * A::K[l] * A::N[l] / 2 + i];
+            for (int i = threadIdx.x; i < A::N[l]; i += NTHR) bi[A::boff(l) + i] = wp[A::woff3(l) + 3 * A::K[l] * A::N[l] / 2 + i];
         for (int j = 0; j < 6; ++j)
-            for (int i = threadIdx.x; i < A::N[2 * j + 1]; i += THREADS)
+            for (int i = threadIdx.x; i < A::N[2 * j + 1]; i += NTHR)
                 bic[cond_off(j) + i] = wp[A::woff3(2 * j + 1) + 3 * A::K[2 * j + 1] * A::N[2 * j + 1] / 2 + i];
-        for (int i = threadIdx.x; i < COND_TOTAL; i += THREADS) cps[i] = CTX ? p.cproj[i] : 0.f;
+        for (int i = threadIdx.x; i < COND_TOTAL; i += NTHR) cps[i] = CTX ? p.cproj[i] : 0.f;
         if (threadIdx.x < CPW) reinterpret_cast<uint32_t *>(lds + L::AMX)[threadIdx.x] = 0u;
         uint32_t am[2] = {0u, 0u};
         // x_T (fp32 + planes)
-        for (int i = threadIdx.x; i < CPW * QUADS; i += THREADS) {
+        for (int i = threadIdx.x; i < CPW * QUADS; i += NTHR) {
             const int c = i / QUADS, qd = i - c * QUADS;
             const int64_t gc = cand0 + c;
             f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -534,8 +583,8 @@ struct MlpX3 {
             store_x(lds, c, qd * 4, z);
         }
 
-        WFrag3<A::K[0], A::N[0], mode_for<A::N[0], R>()> w0;
-        load_w3(w0, W(0), wave, lane16);
+        WFrag3<A::K[0], A::N[0], mode_for<A::N[0], R, W>()> w0;
+        load_w3(w0, wptr(0), wave, lane16);
         f32x4 nz[NZT][NB];
         StepPlan sp = load_plan(p.plan, 0);
         if (wave < 4) fetch_noise(nz, p, sp, 0, cand0, wave, lane);
@@ -561,8 +610,8 @@ struct MlpX3 {
         for (int s = 0; s < p.n_steps; ++s) {
             // launder the weight base: stops LICM hoisting every layer's weight loads out of the loop
             asm volatile("" : "+s"(wofs), "+v"(lane16));
-            WFrag3<A::K[1], A::N[1], mode_for<A::N[1], R>()> w1;
-            load_w3(w1, W(1), wave, lane16);
+            WFrag3<A::K[1], A::N[1], mode_for<A::N[1], R, W>()> w1;
+            load_w3(w1, wptr(1), wave, lane16);
             bar(0);
             // this step's time projections + cond biases (+ shared context part) -> TPU / TPC
             if (threadIdx.x < COND_TOTAL / 4) {
@@ -572,52 +621,52 @@ struct MlpX3 {
             }
             tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 1 < p.n_steps ? s + 1 : s) * COND_TOTAL)[tpi];
             layer<0>(w0, lds, wave, lane);
-            WFrag3<A::K[2], A::N[2], mode_for<A::N[2], R>()> w2;
-            load_w3(w2, W(2), wave, lane16);
+            WFrag3<A::K[2], A::N[2], mode_for<A::N[2], R, W>()> w2;
+            load_w3(w2, wptr(2), wave, lane16);
             bar(1);
             layer<1>(w1, lds, wave, lane);
-            WFrag3<A::K[3], A::N[3], mode_for<A::N[3], R>()> w3;
-            load_w3(w3, W(3), wave, lane16);
+            WFrag3<A::K[3], A::N[3], mode_for<A::N[3], R, W>()> w3;
+            load_w3(w3, wptr(3), wave, lane16);
             bar(2);
             layer<2>(w2, lds, wave, lane);
-            WFrag3<A::K[4], A::N[4], mode_for<A::N[4], R>()> w4;
-            load_w3(w4, W(4), wave, lane16);
+            WFrag3<A::K[4], A::N[4], mode_for<A::N[4], R, W>()> w4;
+            load_w3(w4, wptr(4), wave, lane16);
             bar(3);
             layer<3>(w3, lds, wave, lane);
-            WFrag3<A::K[5], A::N[5], mode_for<A::N[5], R>()> w5;
-            load_w3(w5, W(5), wave, lane16);
+            WFrag3<A::K[5], A::N[5], mode_for<A::N[5], R, W>()> w5;
+            load_w3(w5, wptr(5), wave, lane16);
             bar(4);
             layer<4>(w4, lds, wave, lane);
-            WFrag3<A::K[6], A::N[6], mode_for<A::N[6], R>()> w6;
-            load_w3(w6, W(6), wave, lane16);
+            WFrag3<A::K[6], A::N[6], mode_for<A::N[6], R, W>()> w6;
+            load_w3(w6, wptr(6), wave, lane16);
             bar(5);
             layer<5>(w5, lds, wave, lane);
-            WFrag3<A::K[7], A::N[7], mode_for<A::N[7], R>()> w7;
-            load_w3(w7, W(7), wave, lane16);
+            WFrag3<A::K[7], A::N[7], mode_for<A::N[7], R, W>()> w7;
+            load_w3(w7, wptr(7), wave, lane16);
             bar(6);
             layer<6>(w6, lds, wave, lane);
-            WFrag3<A::K[8], A::N[8], mode_for<A::N[8], R>()> w8;
-            load_w3(w8, W(8), wave, lane16);
+            WFrag3<A::K[8], A::N[8], mode_for<A::N[8], R, W>()> w8;
+            load_w3(w8, wptr(8), wave, lane16);
             bar(7);
             layer<7>(w7, lds, wave, lane);
-            WFrag3<A::K[9], A::N[9], mode_for<A::N[9], R>()> w9;
-            load_w3(w9, W(9), wave, lane16);
+            WFrag3<A::K[9], A::N[9], mode_for<A::N[9], R, W>()> w9;
+            load_w3(w9, wptr(9), wave, lane16);
             bar(8);
             layer<8>(w8, lds, wave, lane);
-            WFrag3<A::K[10], A::N[10], mode_for<A::N[10], R>()> w10;
-            load_w3(w10, W(10), wave, lane16);
+            WFrag3<A::K[10], A::N[10], mode_for<A::N[10], R, W>()> w10;
+            load_w3(w10, wptr(10), wave, lane16);
             bar(9);
             layer<9>(w9, lds, wave, lane);
-            WFrag3<A::K[11], A::N[11], mode_for<A::N[11], R>()> w11;
-            load_w3(w11, W(11), wave, lane16);
+            WFrag3<A::K[11], A::N[11], mode_for<A::N[11], R, W>()> w11;
+            load_w3(w11, wptr(11), wave, lane16);
             bar(10);
             layer<10>(w10, lds, wave, lane);
-            WFrag3<A::K[12], A::N[12], mode_for<A::N[12], R>()> w12;
-            load_w3(w12, W(12), wave, lane16);
+            WFrag3<A::K[12], A::N[12], mode_for<A::N[12], R, W>()> w12;
+            load_w3(w12, wptr(12), wave, lane16);
             bar(11);
             layer<11>(w11, lds, wave, lane);
             FW w13;
-            load_w3(w13, W(13), wave, lane16);
+            load_w3(w13, wptr(13), wave, lane16);
             bar(12);
             layer<12>(w12, lds, wave, lane);
             const StepPlan cur = sp;
@@ -631,13 +680,13 @@ struct MlpX3 {
                 if (wave < 4) fetch_noise(nz, p, sp, s + 1, cand0, wave, lane);
             }
             // next step's layer-0 weights; unconditional (a path-dependent load count drains vmcnt(0))
-            load_w3(w0, W(0), wave, lane16);
+            load_w3(w0, wptr(0), wave, lane16);
             bar(13);
             if (wave < 4) final_and_update(w13, lds, p, cur, s, cand0, nzc, am, wave, lane);
         }
         if (SMODE != MODE_EPS && SMODE != MODE_EPS1 && p.chain_absmax) {
             const int col = lane & 15;
-            store_chain_absmax<CPW, THREADS>(reinterpret_cast<uint32_t *>(lds + L::AMX), am, col,
+            store_chain_absmax<CPW, NTHR>(reinterpret_cast<uint32_t *>(lds + L::AMX), am, col,
                                              (NB == 2 || R == 16) ? -1 : 16 + col,
                                              wave < 4 && (NB == 1 || R == 32 || col < 8), p.chain_absmax, cand0, p.batch);
         }
@@ -645,8 +694,8 @@ struct MlpX3 {
         {
             const uint64_t t = __builtin_readcyclecounter();
             tacc[2 * 15] += t - tprev;
-            if (p.dbg && blockIdx.x < 32 / WAVES && lane == 0)  // 32 wave slots
-                for (int i = 0; i < 32; ++i) p.dbg[(blockIdx.x * WAVES + (threadIdx.x >> 6)) * 32 + i] = (float)tacc[i];
+            if (p.dbg && blockIdx.x < 32 / W && lane == 0)  // 32 wave slots
+                for (int i = 0; i < 32; ++i) p.dbg[(blockIdx.x * W + (threadIdx.x >> 6)) * 32 + i] = (float)tacc[i];
             if (p.dbg && threadIdx.x == 0) {  // per-block loop start / end (memrealtime, low 32 bits)
                 p.dbg[4096 + blockIdx.x * 2] = __builtin_bit_cast(float, (uint32_t)rt0);
                 p.dbg[4096 + blockIdx.x * 2 + 1] = __builtin_bit_cast(float, (uint32_t)__builtin_amdgcn_s_memrealtime());
@@ -660,38 +709,44 @@ struct MlpX3 {
     }
 };
 
-template <int D0, int SMODE, bool CTX, int R>
-__global__ __launch_bounds__(THREADS, 1) void mlp_x3_kernel(const MlpSampleArgs p)
+// (R, W) = (16, 4): 256 threads, two workgroups per CU (two waves per SIMD from independent workgroups)
+template <int D0, int SMODE, bool CTX, int R, int W>
+__global__ __launch_bounds__(64 * W, W == 4 ? 2 : 1) void mlp_x3_kernel(const MlpSampleArgs p)
 {
-    MlpX3<D0, SMODE, CTX, R>::run(p);
+    MlpX3<D0, SMODE, CTX, R, W>::run(p);
 }
 
-template <int D0, int SMODE, bool CTX, int R>
+template <int D0, int SMODE, bool CTX, int R, int W>
 hipError_t launch_x3_r(const MlpSampleArgs &a, hipStream_t stream)
 {
-    using L = Lds3<D0, MlpX3<D0, SMODE, CTX, R>::NB, R>;
+    using L = Lds3<D0, MlpX3<D0, SMODE, CTX, R, W>::NB, R>;
+    static_assert(W == 8 || 2 * L::total <= 160 * 1024, "two 4-wave workgroups per CU");
     static_assert(L::total <= 160 * 1024, "LDS budget (160 KiB per CU)");
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&mlp_x3_kernel<D0, SMODE, CTX, R>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&mlp_x3_kernel<D0, SMODE, CTX, R, W>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     const int64_t blocks = (a.batch + L::CPW - 1) / L::CPW;
-    hipLaunchKernelGGL((mlp_x3_kernel<D0, SMODE, CTX, R>), dim3((unsigned)blocks), dim3(THREADS), (size_t)L::total, stream,
+    hipLaunchKernelGGL((mlp_x3_kernel<D0, SMODE, CTX, R, W>), dim3((unsigned)blocks), dim3(64 * W), (size_t)L::total, stream,
                        a);
     return hipGetLastError();
 }
 
-// 16-row workgroups when 32-row ones would leave CUs idle (fewer than one per CU)
-int mlp_x3_rows(int64_t batch, int nb)
+// Workgroup layout (rows x waves): 32x8 (one per CU), 16x8 when 32-row workgroups would leave CUs idle
+// (fewer than one per CU), 16x4 = two independent 4-wave workgroups per CU, whose barriers and
+// latency chains interleave on each SIMD instead of coinciding. MPCD_MLP_LAYOUT=32x8|16x8|16x4 forces.
+enum { LAYOUT_32x8 = 0, LAYOUT_16x8 = 1, LAYOUT_16x4 = 2 };
+int mlp_x3_layout(int64_t batch, int nb)
 {
     static const int forced = [] {
-        const char *e = getenv("MPCD_MLP_ROWS");
-        return e && e[0] ? atoi(e) : 0;
+        const char *e = getenv("MPCD_MLP_LAYOUT");
+        if (!e || !e[0]) return -1;
+        return !strcmp(e, "32x8") ? (int)LAYOUT_32x8 : !strcmp(e, "16x8") ? (int)LAYOUT_16x8 : !strcmp(e, "16x4") ? (int)LAYOUT_16x4 : -1;
     }();
-    if (forced == 16 || forced == 32) return forced;
+    if (forced >= 0) return forced;
     static int n_cu = 0;
     if (!n_cu) {
         int dev = 0;
@@ -699,15 +754,20 @@ int mlp_x3_rows(int64_t batch, int nb)
             hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             n_cu = 256;
     }
-    return (batch * nb + 31) / 32 < n_cu ? 16 : 32;
+    return (batch * nb + 31) / 32 < n_cu ? LAYOUT_16x8 : LAYOUT_32x8;
 }
 
 template <int D0, int SMODE, bool CTX>
 hipError_t launch_x3(const MlpSampleArgs &a, hipStream_t stream)
 {
     constexpr int NB = MlpX3<D0, SMODE, CTX, 32>::NB;
-    return mlp_x3_rows(a.batch, NB) == 16 ? launch_x3_r<D0, SMODE, CTX, 16>(a, stream)
-                                          : launch_x3_r<D0, SMODE, CTX, 32>(a, stream);
+    switch (mlp_x3_layout(a.batch, NB)) {
+    case LAYOUT_16x8: return launch_x3_r<D0, SMODE, CTX, 16, 8>(a, stream);
+    case LAYOUT_16x4:  // where two 16-row workgroups fit the CU's LDS (else 16x8)
+        if constexpr (2 * Lds3<D0, NB, 16>::total <= 160 * 1024) return launch_x3_r<D0, SMODE, CTX, 16, 4>(a, stream);
+        else return launch_x3_r<D0, SMODE, CTX, 16, 8>(a, stream);
+    default: return launch_x3_r<D0, SMODE, CTX, 32, WAVES>(a, stream);
+    }
 }
 
 template <int D0>

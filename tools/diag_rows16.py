@@ -1,5 +1,5 @@
 """Diagnostics (GPU): the 16-row MLP x3 layout against the 32-row one (eps of both CFG branches) and
-against the oracle, per candidate; MPCD_MLP_ROWS is read once per process, so each layout runs in a
+against the oracle, per candidate; MPCD_MLP_LAYOUT is read once per process, so each layout runs in a
 child process."""
 import os
 import subprocess
@@ -22,8 +22,8 @@ if len(sys.argv) > 1:
     with torch.no_grad():
         rc = net(x, tt, ctx.expand(B, C), torch.zeros(B, 1))
         ru = net(x, tt, ctx.expand(B, C), torch.ones(B, 1))
-    print("rows", os.environ.get("MPCD_MLP_ROWS"), "ec err per cand", [round(float(v), 6) for v in (ec.cpu() - rc).abs().flatten(1).max(1).values],
+    print("layout", os.environ.get("MPCD_MLP_LAYOUT"), "ec err per cand", [round(float(v), 6) for v in (ec.cpu() - rc).abs().flatten(1).max(1).values],
           "eu err per cand", [round(float(v), 6) for v in (eu.cpu() - ru).abs().flatten(1).max(1).values], flush=True)
     sys.exit(0)
-for r in ("32", "16"):
-    subprocess.run([sys.executable, __file__, "x"], env=dict(os.environ, MPCD_MLP_ROWS=r), check=True)
+for r in ("32x8", "16x8", "16x4"):
+    subprocess.run([sys.executable, __file__, "x"], env=dict(os.environ, MPCD_MLP_LAYOUT=r), check=True)
