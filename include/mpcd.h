@@ -240,6 +240,32 @@ int mpcd_comm_init(mpcd_ctx *ctx, int32_t nranks, int32_t rank, const void *id);
  * mpcd_select / mpcd_mpc_step run their N-rank code (rank offsets, gathered-cost order, owner-row sum,
  * flag max-reduction) on one GPU: the single-GPU rehearsal and test of the RCCL path. */
 int mpcd_comm_init_loopback(mpcd_ctx *ctx, int32_t nranks, int32_t rank, uint64_t group_key);
+
+/* ---- native training step: GaussianDiffusionModel.loss / p_losses with CFG context
+ * dropout (diffusion_model_base.py:434-467), WeightedL2 (helpers.py:71-99), backward, torch.optim.Adam
+ * (trainer.py:152) and the EMA model (trainer.py:70-88, 302-308), on the device in fp32. MLP noise-nets
+ * (MPCD_NET_MLP) only. The random draws of p_losses (t ~ randint, noise ~ randn_like, context_mask ~
+ * bernoulli(drop_prob)) are inputs, so a caller reproduces the reference's RNG stream exactly. */
+typedef struct mpcd_trainer mpcd_trainer;
+typedef struct {
+    float lr, beta1, beta2, eps; /* Adam (torch defaults: 0.9, 0.999, 1e-8) */
+    float ema_decay;             /* EMA beta (trainer default 0.995) */
+    int32_t step_start_ema;      /* before this step the EMA model is reset to the model (trainer: 1000) */
+    int32_t update_ema_every;    /* EMA update period in steps (trainer: 10) */
+} mpcd_train_cfg;
+/* params: the net's parameters in mpcd_net_param_info() order; the schedule's sqrt(abar) and
+ * sqrt(1 - abar) [n_steps] (q_sample). The EMA model starts as a copy of params. */
+int mpcd_trainer_create(const mpcd_net_desc *desc, const float *params, size_t n_floats, const mpcd_train_cfg *cfg,
+                        const float *sqrt_alphas_cumprod, const float *sqrt_one_minus_alphas_cumprod, int32_t n_steps,
+                        mpcd_trainer **out);
+/* One batch (device pointers): x0 [B][H*d] normalised trajectories, context [B][C], t [B] (int64, < n_steps),
+ * noise [B][H*d], context_mask [B] (1 = context dropped). update = 0: the loss only (p_losses forward);
+ * 1: loss, backward, Adam step, EMA update. Blocks until done; *loss = mean((eps_pred - noise)^2). */
+int mpcd_trainer_step(mpcd_trainer *tr, const float *x0, const float *context, const int64_t *t, const float *noise,
+                      const float *context_mask, int64_t batch, int32_t update, double *loss, void *hip_stream);
+/* which: 0 parameters, 1 EMA parameters, 2 last gradients, 3 Adam exp_avg, 4 Adam exp_avg_sq (host copy) */
+int mpcd_trainer_params(mpcd_trainer *tr, int32_t which, float *host_out, size_t n_floats);
+void mpcd_trainer_destroy(mpcd_trainer *tr);
 int mpcd_comm_info(mpcd_ctx *ctx, int32_t *nranks, int32_t *rank);  /* 1, 0 without mpcd_comm_init */
 /* recv [nranks * count_per_rank] (rank order); without a communicator: a device copy. */
 int mpcd_allgather_f32(mpcd_ctx *ctx, const float *send, float *recv, size_t count_per_rank, void *hip_stream);

@@ -58,6 +58,11 @@ class StepArgs(ctypes.Structure):
                 ("costs_all", ctypes.c_void_p)]
 
 
+class TrainCfg(ctypes.Structure):
+    _fields_ = [("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float),
+                ("ema_decay", ctypes.c_float), ("step_start_ema", ctypes.c_int32), ("update_ema_every", ctypes.c_int32)]
+
+
 EXPORTS = {
     "mpcd_net_param_count": ([ctypes.POINTER(NetDesc), ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)],
                              ctypes.c_int),
@@ -110,6 +115,14 @@ EXPORTS = {
     "mpcd_allreduce_max_i32": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
     "mpcd_mpc_step": ([ctypes.c_void_p, ctypes.POINTER(StepArgs), ctypes.POINTER(Best), ctypes.c_void_p,
                        ctypes.c_void_p], ctypes.c_int),
+    "mpcd_trainer_create": ([ctypes.POINTER(NetDesc), ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(TrainCfg),
+                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)],
+                            ctypes.c_int),
+    "mpcd_trainer_step": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                           ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_double),
+                           ctypes.c_void_p], ctypes.c_int),
+    "mpcd_trainer_params": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t], ctypes.c_int),
+    "mpcd_trainer_destroy": ([ctypes.c_void_p], None),
     "mpcd_select": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
 }

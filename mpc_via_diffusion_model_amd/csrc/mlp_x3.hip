@@ -48,6 +48,9 @@ constexpr int ROWS_MAX = 32;
 #ifndef MPCD_X3_PAIR_MIN
 #define MPCD_X3_PAIR_MIN 128
 #endif
+#ifndef MPCD_X3_XALL
+#define MPCD_X3_XALL 0
+#endif
 #ifndef MPCD_X3_ILV
 #define MPCD_X3_ILV 1
 #endif
@@ -355,6 +358,14 @@ struct MlpX3 {
                 load_x3(x, lds + L::in_off(l) + (c * 16 + col) * L::in_rs(l) + (kc * 32 + 8 * q) * 2, L::in_pl(l));
             };
             auto chain = [&](int c) {
+#if MPCD_X3_XALL
+                // every k-chunk's fragments first: one LDS round trip per chain instead of one per chunk
+                u32x4 xk[KC][3];
+#pragma unroll
+                for (int kc = 0; kc < KC; ++kc) ldx1(xk[kc], c, kc);
+#pragma unroll
+                for (int kc = 0; kc < KC; ++kc) acc[0][c] = mfma_x3(f.v[0][kc], xk[kc], acc[0][c]);
+#else
                 u32x4 xa[3], xb[3];
                 ldx1(xa, c, 0);
 #pragma unroll
@@ -362,6 +373,7 @@ struct MlpX3 {
                     if (kc + 1 < KC) ldx1((kc & 1) ? xa : xb, c, kc + 1);
                     acc[0][c] = mfma_x3(f.v[0][kc], (kc & 1) ? xb : xa, acc[0][c]);
                 }
+#endif
             };
             chain(0);
             __builtin_amdgcn_sched_barrier(0);

@@ -14,6 +14,9 @@
 
 #include "../../include/mpcd.h"
 #include "comm.h"
+#include "train.h"
+
+#include <map>
 #include "internal.h"
 #include "unet.h"
 
@@ -1086,6 +1089,117 @@ int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, fl
                     code == 2 ? "; NaN in the sampled trajectories" : "");
     }
     return MPCD_OK;
+}
+
+
+// ---- native training step: MLP noise-net, fp32, csrc/train.hip
+
+struct mpcd_trainer {
+    Trainer *t = nullptr;
+    int64_t n_params = 0;
+};
+
+int mpcd_trainer_create(const mpcd_net_desc *desc, const float *params, size_t n_floats, const mpcd_train_cfg *cfg,
+                        const float *sqrt_alphas_cumprod, const float *sqrt_one_minus_alphas_cumprod, int32_t n_steps,
+                        mpcd_trainer **out)
+{
+    if (!out) return fail(MPCD_EINVAL, "null out");
+    *out = nullptr;
+    if (int r = check_desc(desc)) return r;
+    if (desc->kind != MPCD_NET_MLP || desc->dtype == MPCD_F16)
+        return fail(MPCD_EUNSUP, "mpcd_trainer: the CFG MLP noise-net in fp32 only");
+    if (!params || !cfg || !sqrt_alphas_cumprod || !sqrt_one_minus_alphas_cumprod || n_steps < 1)
+        return fail(MPCD_EINVAL, "mpcd_trainer_create: null argument or no schedule");
+    const std::vector<PSpec> spec = param_spec(*desc);
+    std::map<std::string, int64_t> off;
+    int64_t o = 0;
+    for (const PSpec &p : spec) {
+        off[p.name] = o;
+        o += p.numel();
+    }
+    if ((size_t)o != n_floats) return fail(MPCD_EINVAL, "mpcd_trainer_create: %zu floats, the net has %lld", n_floats, (long long)o);
+    auto lin = [&](const std::string &pre, int n, int k) {
+        TrainLin L;
+        L.w = off.at(pre + ".weight");
+        L.b = off.at(pre + ".bias");
+        L.n = n;
+        L.k = k;
+        return L;
+    };
+    TrainSpec sp;
+    sp.flat = desc->horizon * desc->state_dim;
+    sp.temb = desc->time_emb_dim;
+    sp.ctx_dim = desc->context_dim;
+    sp.base = desc->base_dim;
+    sp.n_steps = n_steps;
+    sp.n_params = o;
+    sp.lr = cfg->lr;
+    sp.beta1 = cfg->beta1;
+    sp.beta2 = cfg->beta2;
+    sp.eps = cfg->eps;
+    sp.ema_decay = cfg->ema_decay;
+    sp.step_start_ema = cfg->step_start_ema;
+    sp.update_ema_every = cfg->update_ema_every;
+    const int cond = cond_dim_of(*desc);
+    sp.t1 = lin("time_mlp.encoder.1", 128, 32);
+    sp.t2 = lin("time_mlp.encoder.3", desc->time_emb_dim, 128);
+    auto st = stages(sp.flat, *desc);
+    const int ns = (int)st.size();
+    auto block = [&](const std::string &p, int ci, int co, int in0, int in1) {
+        TrainBlock b;
+        b.la = lin(p + ".blocks.0._network.0", co, ci);
+        b.lb = lin(p + ".blocks.0._network.2", co, co);
+        b.lc = lin(p + ".cond_mlp.1", co, cond);
+        b.co = co;
+        b.in0 = in0;
+        b.in1 = in1;
+        return b;
+    };
+    for (int i = 0; i < ns; ++i) sp.blocks.push_back(block("downs." + std::to_string(i) + ".0", st[i].first, st[i].second, i - 1, -1));
+    sp.blocks.push_back(block("mid_block1", st.back().second, st.back().second, ns - 1, -1));
+    for (int i = 1; i < ns; ++i) {  // ups.{i-1}: cat(previous output, skip = downs.{ns-i})
+        auto [ci, co] = st[ns - i];
+        sp.blocks.push_back(block("ups." + std::to_string(i - 1) + ".0", 2 * co, ci, (int)sp.blocks.size() - 1, ns - i));
+    }
+    sp.f1 = lin("final_layer.0._network.0", desc->base_dim, desc->base_dim);
+    sp.f2 = lin("final_layer.0._network.2", sp.flat, desc->base_dim);
+    std::vector<float> sched((size_t)2 * n_steps);
+    std::copy(sqrt_alphas_cumprod, sqrt_alphas_cumprod + n_steps, sched.begin());
+    std::copy(sqrt_one_minus_alphas_cumprod, sqrt_one_minus_alphas_cumprod + n_steps, sched.begin() + n_steps);
+    std::string why;
+    Trainer *t = trainer_new(sp, params, sched.data(), &why);
+    if (!t) return fail(MPCD_ENOMEM, "%s", why.c_str());
+    *out = new mpcd_trainer{t, o};
+    return MPCD_OK;
+}
+
+int mpcd_trainer_step(mpcd_trainer *tr, const float *x0, const float *context, const int64_t *t, const float *noise,
+                      const float *context_mask, int64_t batch, int32_t update, double *loss, void *hip_stream)
+{
+    if (!tr || !x0 || !context || !t || !noise || !context_mask || !loss || batch < 1)
+        return fail(MPCD_EINVAL, "mpcd_trainer_step: null argument or empty batch");
+    TrainBatch b{x0, context, noise, context_mask, t, batch, hip_stream};
+    std::string why;
+    const int r = trainer_step(tr->t, b, update != 0, loss, &why);
+    if (r == -1) return fail(MPCD_ENOMEM, "%s", why.c_str());
+    if (r != 0) return fail(MPCD_EHIP, "%s", why.c_str());
+    return MPCD_OK;
+}
+
+int mpcd_trainer_params(mpcd_trainer *tr, int32_t which, float *host_out, size_t n_floats)
+{
+    if (!tr || !host_out || which < 0 || which > 4) return fail(MPCD_EINVAL, "mpcd_trainer_params: bad argument");
+    const int r = trainer_read(tr->t, which, host_out, n_floats);
+    if (r == -1) return fail(MPCD_EINVAL, "mpcd_trainer_params: %zu floats, the net has %lld", n_floats, (long long)tr->n_params);
+    if (r != 0) return fail(MPCD_EHIP, "mpcd_trainer_params: copy failed");
+    return MPCD_OK;
+}
+
+void mpcd_trainer_destroy(mpcd_trainer *tr)
+{
+    if (!tr) return;
+    trainer_free(tr->t);
+    delete tr;
 }
 
 }  // extern "C"

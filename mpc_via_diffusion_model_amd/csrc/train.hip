@@ -1,0 +1,447 @@
+// Native training step for the CFG MLP noise-net: GaussianDiffusionModel.p_losses
+// with CFG context dropout (mpd/models/diffusion_models/diffusion_model_base.py:434-467), the WeightedL2
+// loss (helpers.py:71-99), backward through every layer, torch.optim.Adam (trainer.py:152) and the
+// EMA model update (trainer.py:70-88, 302-308), all on the device in fp32.
+//
+// Training is offline and sized by the training batch (thousands of rows, widths <= 256), so the
+// GEMMs are one LDS-tiled fp32 kernel with generic operand strides (Y = X W^T, dX = dY W, dW = dY^T X
+// and the bias gradients as dY^T 1), and everything else is elementwise. Activations of the forward
+// pass stay in HBM for the backward pass ([rows][width] row-major, one buffer per tensor).
+//
+// Net (oracle/nets.py ConditionedMLPNet = temporal_unet.py PointUnet stack with a CFG context):
+//   t_emb = L_t2(Mish(L_t1(sinemb(t))));  c = cat(t_emb, ctx * (1 - mask));  mc = Mish(c)
+//   block(x) = Mish(L_b(Mish(L_a x)) + L_c mc)      (TemporalBlockMLP, layers.py:358-385)
+//   downs d0..d{n-1}, mid, ups u_k(cat(y, d_{n-2-k})), out = L_f2(L_f1 y)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "train.h"
+
+namespace {
+
+constexpr int GT = 64;   // GEMM tile (rows and columns of C per workgroup)
+constexpr int GK = 16;   // k-step staged in LDS
+
+// C[m][n] (ldc) = beta * C + sum_k A(m,k) B(k,n) (+ bias[n]); A(m,k) = a[m*sam + k*sak], B(k,n) = b[k*sbk + n*sbn].
+// 256 threads, each a 4x4 block of C; the k-sum runs in k order per output (fp32 FMA off: -ffp-contract=off).
+__global__ __launch_bounds__(256) void gemm_kernel(int M, int N, int K, const float *__restrict__ a, int64_t sam,
+                                                   int64_t sak, const float *__restrict__ b, int64_t sbk, int64_t sbn,
+                                                   float *__restrict__ c, int64_t ldc, float beta,
+                                                   const float *__restrict__ bias)
+{
+    __shared__ float As[GK][GT + 1], Bs[GK][GT + 1];
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
+    float acc[4][4] = {};
+    for (int k0 = 0; k0 < K; k0 += GK) {
+        for (int i = threadIdx.x; i < GK * GT; i += 256) {
+            const int kk = i / GT, r = i % GT;
+            const int m = m0 + r, n = n0 + r, k = k0 + kk;
+            As[kk][r] = (m < M && k < K) ? a[m * sam + k * sak] : 0.f;
+            Bs[kk][r] = (n < N && k < K) ? b[k * sbk + n * sbn] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < GK; ++kk) {
+            float av[4], bv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                av[i] = As[kk][ty + 16 * i];
+                bv[i] = Bs[kk][tx + 16 * i];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] += av[i] * bv[j];
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = m0 + ty + 16 * i;
+        if (m >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + tx + 16 * j;
+            if (n >= N) continue;
+            float v = acc[i][j];
+            if (bias) v += bias[n];
+            float *p = c + m * ldc + n;
+            *p = beta != 0.f ? *p + v : v;
+        }
+    }
+}
+
+MPCD_DEV float softplus(float x) { return log1pf(expf(x)); }  // as torch's Mish kernels (no threshold)
+
+// Mish forward (torch: x * tanh(softplus(x)))
+__global__ void mish_fwd_kernel(int64_t n, const float *__restrict__ pre, float *__restrict__ out)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = pre[i] * tanhf(softplus(pre[i]));
+}
+
+// d pre = d out * (tanh(sp) + x * sigmoid(x) * (1 - tanh(sp)^2))  (torch's Mish backward); in place allowed
+__global__ void mish_bwd_kernel(int64_t n, const float *__restrict__ pre, const float *dout, float *dpre)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float x = pre[i];
+        const float tsp = tanhf(softplus(x));
+        const float sg = 1.f / (1.f + expf(-x));
+        dpre[i] = dout[i] * (tsp + x * sg * (1.f - tsp * tsp));
+    }
+}
+
+// x_noisy = sqrt(abar_t) x0 + sqrt(1 - abar_t) noise  (q_sample, diffusion_model_base.py:421-431)
+__global__ void q_sample_kernel(int64_t B, int F, const float *x0, const float *noise, const int64_t *t,
+                                const float *sac, const float *s1mac, float *xn)
+{
+    const int64_t n = B * F;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t ti = t[i / F];
+        const float u = sac[ti] * x0[i], v = s1mac[ti] * noise[i];
+        xn[i] = u + v;
+    }
+}
+
+// SinusoidalPosEmb(32) (layers.py:249-255): [sin(t f_k), cos(t f_k)], f_k = exp(k * -(ln 1e4 / 15))
+__global__ void sinemb_kernel(int64_t B, const int64_t *t, float *e)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < B * 32; i += (int64_t)gridDim.x * blockDim.x) {
+        const int j = (int)(i & 31), k = j & 15;
+        const float f = expf((float)k * (float)(-(9.210340371976184 / 15.0)));
+        const float arg = (float)t[i >> 5] * f;
+        e[i] = j < 16 ? sinf(arg) : cosf(arg);
+    }
+}
+
+// c_emb = cat(t_emb, ctx * (1 - mask))  (ConditionedMLPNet.forward)
+__global__ void cemb_kernel(int64_t B, int T, int C, const float *temb, const float *ctx, const float *mask, float *c)
+{
+    const int W = T + C;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < B * W; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = i / W;
+        const int j = (int)(i - b * W);
+        c[i] = j < T ? temb[b * T + j] : ctx[b * C + (j - T)] * (1.f - mask[b]);
+    }
+}
+
+// loss partials: sum (o - n)^2 per block (fp64), and d out = 2 (o - n) / numel
+__global__ __launch_bounds__(256) void l2_kernel(int64_t n, const float *o, const float *y, float inv_n, float *dout,
+                                                 double *part)
+{
+    __shared__ double s[256];
+    double acc = 0.0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float d = o[i] - y[i];
+        acc += (double)(d * d);
+        if (dout) dout[i] = (2.f * d) * inv_n;
+    }
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = s[0];
+}
+
+// bias gradient db[n] += sum_m dy[m*ld + n]: 64 columns per workgroup, 4 row lanes, fixed order
+__global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int N, const float *dy, int64_t ld, float *db)
+{
+    __shared__ float s[4][64];
+    const int c = threadIdx.x & 63, r = threadIdx.x >> 6, n = blockIdx.x * 64 + c;
+    float acc = 0.f;
+    if (n < N)
+        for (int64_t m = r; m < M; m += 4) acc += dy[m * ld + n];
+    s[r][c] = acc;
+    __syncthreads();
+    if (r == 0 && n < N) db[n] += (s[0][c] + s[1][c]) + (s[2][c] + s[3][c]);
+}
+
+// torch.optim.Adam single-tensor step (no weight decay, no amsgrad)
+__global__ void adam_kernel(int64_t n, float *p, const float *g, float *m, float *v, float b1, float b2, float step_size,
+                            float bc2_sqrt, float eps)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float gi = g[i];
+        m[i] = m[i] + (1.f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1 - beta1)
+        v[i] = v[i] * b2 + (1.f - b2) * gi * gi;
+        const float denom = sqrtf(v[i]) / bc2_sqrt + eps;
+        p[i] = p[i] + (-step_size) * (m[i] / denom);
+    }
+}
+
+// EMA.update_average: old * beta + (1 - beta) * new
+__global__ void ema_kernel(int64_t n, float *ema, const float *p, float beta, int reset)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float old = reset ? p[i] : ema[i];
+        ema[i] = old * beta + (1.f - beta) * p[i];
+    }
+}
+
+unsigned grid_for(int64_t n) { return (unsigned)std::min<int64_t>((n + 255) / 256, 4096); }
+
+}  // namespace
+
+struct Trainer {
+    TrainSpec sp;
+    hipStream_t st = nullptr;
+    int64_t cap = 0;  // rows the activation buffers hold
+    float *P = nullptr, *G = nullptr, *Mo = nullptr, *Vo = nullptr, *E = nullptr, *sched = nullptr;
+    std::vector<float *> bufs;
+    double *part = nullptr;
+    int64_t step = 0;
+
+    ~Trainer()
+    {
+        for (float *b : bufs) (void)hipFree(b);
+        for (float *b : {P, G, Mo, Vo, E, sched}) (void)hipFree(b);
+        (void)hipFree(part);
+    }
+    float *alloc(int64_t n)
+    {
+        float *p = nullptr;
+        if (hipMalloc(&p, (size_t)std::max<int64_t>(n, 1) * 4) != hipSuccess) return nullptr;
+        bufs.push_back(p);
+        return p;
+    }
+    hipError_t gemm(int M, int N, int K, const float *a, int64_t sam, int64_t sak, const float *b, int64_t sbk,
+                    int64_t sbn, float *c, int64_t ldc, float beta, const float *bias)
+    {
+        dim3 g((N + GT - 1) / GT, (M + GT - 1) / GT);
+        hipLaunchKernelGGL(gemm_kernel, g, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, c, ldc, beta, bias);
+        return hipGetLastError();
+    }
+    // Y[B][N] = X[B][K] W[N][K]^T + b   (X rows of stride ldx; W rows of stride ldw, starting at column koff)
+    hipError_t lin(int64_t B, const float *x, int ldx, const TrainLin &L, int koff, int K, float *y, float beta, bool bias)
+    {
+        return gemm((int)B, L.n, K, x, ldx, 1, P + L.w + koff, 1, L.k, y, L.n, beta, bias ? P + L.b : nullptr);
+    }
+    // backward of Y = X W[:, koff:koff+K]^T: dW[:, koff..] += dY^T X; dX (+)= dY W[:, koff..]
+    hipError_t lin_bwd(int64_t B, const float *x, int ldx, const TrainLin &L, int koff, int K, const float *dy, float *dx,
+                       float dx_beta)
+    {
+        hipError_t e = gemm(L.n, K, (int)B, dy, 1, L.n, x, ldx, 1, G + L.w + koff, L.k, 1.f, nullptr);
+        if (e == hipSuccess && dx) e = gemm((int)B, K, L.n, dy, L.n, 1, P + L.w + koff, L.k, 1, dx, K, dx_beta, nullptr);
+        return e;
+    }
+    hipError_t bias_bwd(int64_t B, const TrainLin &L, const float *dy)
+    {
+        hipLaunchKernelGGL(colsum_kernel, dim3((L.n + 63) / 64), dim3(256), 0, st, B, L.n, dy, (int64_t)L.n, G + L.b);
+        return hipGetLastError();
+    }
+    void mish(int64_t n, const float *pre, float *out)
+    {
+        hipLaunchKernelGGL(mish_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, pre, out);
+    }
+    void mish_bwd(int64_t n, const float *pre, const float *dout, float *dpre)
+    {
+        hipLaunchKernelGGL(mish_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, pre, dout, dpre);
+    }
+
+    // activation buffers per training row count
+    struct Act {
+        float *xn, *e, *p1, *q1, *temb, *cemb, *mc, *f1, *out, *dout, *dmc, *dcemb, *dq1, *tmp;
+        std::vector<float *> a1, h1, s, y, dy, dh;  // per block
+    } A{};
+
+    int reserve(int64_t B)
+    {
+        if (B <= cap) return 0;
+        for (float *b : bufs) (void)hipFree(b);
+        bufs.clear();
+        const int F = sp.flat, T = sp.temb, W = sp.temb + sp.ctx_dim, nb = (int)sp.blocks.size();
+        A.xn = alloc(B * F);
+        A.e = alloc(B * 32);
+        A.p1 = alloc(B * 128);
+        A.q1 = alloc(B * 128);
+        A.temb = alloc(B * T);
+        A.cemb = alloc(B * W);
+        A.mc = alloc(B * W);
+        A.f1 = alloc(B * sp.base);
+        A.out = alloc(B * F);
+        A.dout = alloc(B * F);
+        A.dmc = alloc(B * W);
+        A.dcemb = alloc(B * W);
+        A.dq1 = alloc(B * 128);
+        A.tmp = alloc(B * 256);
+        A.a1.assign(nb, nullptr);
+        A.h1 = A.s = A.y = A.dy = A.dh = A.a1;
+        for (int j = 0; j < nb; ++j) {
+            const int co = sp.blocks[j].co;
+            A.a1[j] = alloc(B * co);
+            A.h1[j] = alloc(B * co);
+            A.s[j] = alloc(B * co);
+            A.y[j] = alloc(B * co);
+            A.dy[j] = alloc(B * co);
+            A.dh[j] = alloc(B * co);
+        }
+        for (float *b : bufs)
+            if (!b) return -1;
+        cap = B;
+        return 0;
+    }
+
+    // block j's input: x_noisy (first down), the previous block's output, or the concat (y_prev, skip)
+    hipError_t block_fwd(int64_t B, int j)
+    {
+        const TrainBlock &k = sp.blocks[j];
+        hipError_t e;
+        const float *x0 = k.in0 < 0 ? A.xn : A.y[k.in0];
+        const int c0 = k.in0 < 0 ? sp.flat : sp.blocks[k.in0].co;
+        e = lin(B, x0, c0, k.la, 0, c0, A.a1[j], 0.f, true);
+        if (e == hipSuccess && k.in1 >= 0) e = lin(B, A.y[k.in1], sp.blocks[k.in1].co, k.la, c0, sp.blocks[k.in1].co, A.a1[j], 1.f, false);
+        if (e != hipSuccess) return e;
+        mish(B * k.co, A.a1[j], A.h1[j]);
+        e = lin(B, A.h1[j], k.co, k.lb, 0, k.co, A.s[j], 0.f, true);
+        if (e == hipSuccess) e = lin(B, A.mc, sp.temb + sp.ctx_dim, k.lc, 0, sp.temb + sp.ctx_dim, A.s[j], 1.f, true);
+        if (e != hipSuccess) return e;
+        mish(B * k.co, A.s[j], A.y[j]);
+        return hipGetLastError();
+    }
+    // given dy[j] (gradient of block j's output), accumulate parameter grads, dmc, and the inputs' grads
+    hipError_t block_bwd(int64_t B, int j)
+    {
+        const TrainBlock &k = sp.blocks[j];
+        const int W = sp.temb + sp.ctx_dim;
+        hipError_t e;
+        mish_bwd(B * k.co, A.s[j], A.dy[j], A.dh[j]);  // d s
+        e = bias_bwd(B, k.lb, A.dh[j]);
+        if (e == hipSuccess) e = bias_bwd(B, k.lc, A.dh[j]);
+        if (e == hipSuccess) e = lin_bwd(B, A.mc, W, k.lc, 0, W, A.dh[j], A.dmc, 1.f);
+        if (e == hipSuccess) e = lin_bwd(B, A.h1[j], k.co, k.lb, 0, k.co, A.dh[j], A.tmp, 0.f);  // d h1 -> tmp
+        if (e != hipSuccess) return e;
+        mish_bwd(B * k.co, A.a1[j], A.tmp, A.tmp);  // d a1
+        e = bias_bwd(B, k.la, A.tmp);
+        if (e != hipSuccess) return e;
+        const float *x0 = k.in0 < 0 ? A.xn : A.y[k.in0];
+        const int c0 = k.in0 < 0 ? sp.flat : sp.blocks[k.in0].co;
+        e = lin_bwd(B, x0, c0, k.la, 0, c0, A.tmp, k.in0 < 0 ? nullptr : A.dy[k.in0], 1.f);
+        if (e == hipSuccess && k.in1 >= 0)
+            e = lin_bwd(B, A.y[k.in1], sp.blocks[k.in1].co, k.la, c0, sp.blocks[k.in1].co, A.tmp, A.dy[k.in1], 1.f);
+        return e;
+    }
+
+    hipError_t run(int64_t B, const float *x0, const float *ctx, const int64_t *t, const float *noise, const float *mask,
+                   bool update, double *loss)
+    {
+        const int F = sp.flat, T = sp.temb, C = sp.ctx_dim, W = T + C;
+        const int nb = (int)sp.blocks.size();
+        hipError_t e;
+        // ---- forward (p_losses)
+        hipLaunchKernelGGL(q_sample_kernel, dim3(grid_for(B * F)), dim3(256), 0, st, B, F, x0, noise, t, sched,
+                           sched + sp.n_steps, A.xn);
+        hipLaunchKernelGGL(sinemb_kernel, dim3(grid_for(B * 32)), dim3(256), 0, st, B, t, A.e);
+        if ((e = lin(B, A.e, 32, sp.t1, 0, 32, A.p1, 0.f, true)) != hipSuccess) return e;
+        mish(B * 128, A.p1, A.q1);
+        if ((e = lin(B, A.q1, 128, sp.t2, 0, 128, A.temb, 0.f, true)) != hipSuccess) return e;
+        hipLaunchKernelGGL(cemb_kernel, dim3(grid_for(B * W)), dim3(256), 0, st, B, T, C, A.temb, ctx, mask, A.cemb);
+        mish(B * W, A.cemb, A.mc);
+        for (int j = 0; j < nb; ++j)
+            if ((e = block_fwd(B, j)) != hipSuccess) return e;
+        const int last = nb - 1;
+        if ((e = lin(B, A.y[last], sp.base, sp.f1, 0, sp.base, A.f1, 0.f, true)) != hipSuccess) return e;
+        if ((e = lin(B, A.f1, sp.base, sp.f2, 0, sp.base, A.out, 0.f, true)) != hipSuccess) return e;
+        // ---- loss = mean((eps - noise)^2)  (WeightedL2, predict_epsilon)
+        const int64_t n = B * F;
+        const unsigned nbk = std::min<unsigned>(grid_for(n), 1024);
+        hipLaunchKernelGGL(l2_kernel, dim3(nbk), dim3(256), 0, st, n, A.out, noise, (float)(1.0 / (double)n),
+                           update ? A.dout : nullptr, part);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        std::vector<double> hp(nbk);
+        if ((e = hipMemcpyAsync(hp.data(), part, nbk * sizeof(double), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        if (!update) {
+            if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+            double s = 0;
+            for (double v : hp) s += v;
+            *loss = s / (double)n;
+            return hipSuccess;
+        }
+        // ---- backward
+        if ((e = hipMemsetAsync(G, 0, (size_t)sp.n_params * 4, st)) != hipSuccess) return e;
+        for (int j = 0; j < nb; ++j)
+            if ((e = hipMemsetAsync(A.dy[j], 0, (size_t)B * sp.blocks[j].co * 4, st)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(A.dmc, 0, (size_t)B * W * 4, st)) != hipSuccess) return e;
+        if ((e = bias_bwd(B, sp.f2, A.dout)) != hipSuccess) return e;
+        if ((e = lin_bwd(B, A.f1, sp.base, sp.f2, 0, sp.base, A.dout, A.tmp, 0.f)) != hipSuccess) return e;  // d f1
+        if ((e = bias_bwd(B, sp.f1, A.tmp)) != hipSuccess) return e;
+        if ((e = lin_bwd(B, A.y[last], sp.base, sp.f1, 0, sp.base, A.tmp, A.dy[last], 1.f)) != hipSuccess) return e;
+        for (int j = nb - 1; j >= 0; --j)
+            if ((e = block_bwd(B, j)) != hipSuccess) return e;
+        mish_bwd(B * W, A.cemb, A.dmc, A.dcemb);
+        // time MLP: d t_emb = d c_emb[:, :T] (row stride W)
+        if ((e = gemm(sp.t2.n, 128, (int)B, A.dcemb, 1, W, A.q1, 128, 1, G + sp.t2.w, 128, 1.f, nullptr)) != hipSuccess) return e;
+        hipLaunchKernelGGL(colsum_kernel, dim3((T + 63) / 64), dim3(256), 0, st, B, T, A.dcemb, (int64_t)W, G + sp.t2.b);
+        if ((e = gemm((int)B, 128, T, A.dcemb, W, 1, P + sp.t2.w, 128, 1, A.dq1, 128, 0.f, nullptr)) != hipSuccess) return e;
+        mish_bwd(B * 128, A.p1, A.dq1, A.dq1);
+        if ((e = bias_bwd(B, sp.t1, A.dq1)) != hipSuccess) return e;
+        if ((e = lin_bwd(B, A.e, 32, sp.t1, 0, 32, A.dq1, nullptr, 0.f)) != hipSuccess) return e;
+        // ---- Adam, then the EMA model (trainer.py: optimizer step, then every update_ema_every steps)
+        ++step;
+        const double bc1 = 1.0 - std::pow((double)sp.beta1, (double)step), bc2 = 1.0 - std::pow((double)sp.beta2, (double)step);
+        hipLaunchKernelGGL(adam_kernel, dim3(grid_for(sp.n_params)), dim3(256), 0, st, (int64_t)sp.n_params, P, G, Mo, Vo,
+                           sp.beta1, sp.beta2, (float)(sp.lr / bc1), (float)std::sqrt(bc2), sp.eps);
+        const int64_t s0 = step - 1;  // trainer's train_steps_current before its increment
+        if (sp.update_ema_every > 0 && s0 % sp.update_ema_every == 0)
+            hipLaunchKernelGGL(ema_kernel, dim3(grid_for(sp.n_params)), dim3(256), 0, st, (int64_t)sp.n_params, E, P,
+                               sp.ema_decay, s0 < sp.step_start_ema ? 1 : 0);
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+        double s = 0;
+        for (double v : hp) s += v;
+        *loss = s / (double)n;
+        return hipGetLastError();
+    }
+};
+
+Trainer *trainer_new(const TrainSpec &sp, const float *params_host, const float *sched_host, std::string *why)
+{
+    Trainer *t = new Trainer;
+    t->sp = sp;
+    const size_t pb = (size_t)sp.n_params * 4;
+    bool ok = hipMalloc(&t->P, pb) == hipSuccess && hipMalloc(&t->G, pb) == hipSuccess &&
+              hipMalloc(&t->Mo, pb) == hipSuccess && hipMalloc(&t->Vo, pb) == hipSuccess &&
+              hipMalloc(&t->E, pb) == hipSuccess && hipMalloc(&t->sched, (size_t)sp.n_steps * 2 * 4) == hipSuccess &&
+              hipMalloc(&t->part, 1024 * sizeof(double)) == hipSuccess;
+    ok = ok && hipMemcpy(t->P, params_host, pb, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(t->E, params_host, pb, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemset(t->Mo, 0, pb) == hipSuccess && hipMemset(t->Vo, 0, pb) == hipSuccess &&
+         hipMemset(t->G, 0, pb) == hipSuccess &&
+         hipMemcpy(t->sched, sched_host, (size_t)sp.n_steps * 2 * 4, hipMemcpyHostToDevice) == hipSuccess;
+    if (!ok) {
+        if (why) *why = "trainer: device allocation / upload failed";
+        delete t;
+        return nullptr;
+    }
+    return t;
+}
+
+int trainer_step(Trainer *t, const TrainBatch &b, bool update, double *loss, std::string *why)
+{
+    t->st = (hipStream_t)b.stream;
+    if (t->reserve(b.batch) != 0) {
+        if (why) *why = "trainer: activation buffers";
+        return -1;
+    }
+    const hipError_t e = t->run(b.batch, b.x0, b.ctx, b.t, b.noise, b.mask, update, loss);
+    if (e != hipSuccess) {
+        if (why) *why = std::string("trainer: ") + hipGetErrorString(e);
+        return -2;
+    }
+    return 0;
+}
+
+int trainer_read(Trainer *t, int which, float *host, size_t n)
+{
+    if (n != (size_t)t->sp.n_params) return -1;
+    const float *src = which == 0 ? t->P : which == 1 ? t->E : which == 2 ? t->G : which == 3 ? t->Mo : t->Vo;
+    return hipMemcpy(host, src, n * 4, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
+
+int64_t trainer_steps(Trainer *t) { return t->step; }
+
+void trainer_free(Trainer *t) { delete t; }

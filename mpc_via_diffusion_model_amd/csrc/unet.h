@@ -60,6 +60,11 @@ struct ConvMK {
     // fp16 activation buffers (f16 net): input (xa / xb), residual, output hold halves, not floats
     int in_h, res_h, out_h;
     int layer;              // index of the conv in UnetWeights::layers (diagnostics)
+    // first-generation stagger (non-persistent grids): workgroup b < stag_ncu * stag_slots sleeps
+    // (b / stag_ncu) * stag_units x s_sleep(32), so the co-resident workgroups of a CU run their
+    // staging / GEMM / epilogue phases out of step instead of all at once
+    int stag_units, stag_ncu, stag_slots;
+    uint32_t *wgtrace;      // diagnostics (MPCD_UNET_WGTRACE): per workgroup {start, end, HW_ID, XCC_ID}
 };
 
 struct UnetWeights {

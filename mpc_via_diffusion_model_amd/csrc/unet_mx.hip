@@ -52,6 +52,11 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int MT = 256;  // threads per workgroup
+// weight chunks in flight for the small f16 tiles (NN x NC <= 8): the GEMM phase of a 4-row block
+// streams the whole layer's weights from L2 for 64 columns, so its A loads are latency-bound
+#ifndef MPCD_MX_DA_SMALL
+#define MPCD_MX_DA_SMALL 4
+#endif
 
 MPCD_DEV uint32_t pk_bf16(float lo, float hi)
 {
@@ -182,6 +187,14 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
     extern __shared__ __attribute__((aligned(16))) char sm[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    if constexpr (!PERS) {
+        const ConvMK &a0 = as.ph[0];
+        if (a0.stag_units > 0 && (int64_t)blockIdx.x < (int64_t)a0.stag_ncu * a0.stag_slots) {
+            const int n = (int)(blockIdx.x / (unsigned)a0.stag_ncu) * a0.stag_units;
+            for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(32);
+        }
+    }
     static_assert(NPH == 1 || (!PERS && KIND == UCONV_SAME5), "fused pairs: 5-tap convs, one row block per workgroup");
     if constexpr (NPH == 2) {  // zero the halo positions of the second conv's staging window (rows rb)
         const ConvMK &a = as.ph[0];
@@ -399,7 +412,7 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
         // A (weights, L2) runs DA chunks ahead in a register ring; B (LDS) one chunk ahead. The
         // prefetches are unconditional (clamped to the last chunk) so the waits before each chunk's
         // MFMAs leave the younger loads in flight.
-        constexpr int DA = P == 1 ? (NN * NC >= 32 ? 2 : 4) : 2;
+        constexpr int DA = P == 1 ? (NN * NC >= 32 ? 2 : NN * NC >= 16 ? 4 : MPCD_MX_DA_SMALL) : 2;
         u32x4 A[DA][NN][P];
 #pragma unroll
         for (int s = 0; s < DA; ++s) load_a(A[s], min(s, KC - 1));
@@ -644,6 +657,14 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
     }
     if (ph + 1 < NPH) __syncthreads();  // the second conv's planes complete; tile / statistics free
     }
+    if (as.ph[0].wgtrace && tid == 0) {  // diagnostics: workgroup residency (vector stores from lane 0)
+        const uint32_t t_end = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        uint32_t *tr = as.ph[0].wgtrace + 4 * (size_t)blockIdx.x;
+        tr[0] = t_start;
+        tr[1] = t_end;
+        tr[2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID: wave, SIMD, CU, SH, SE
+        tr[3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    }
 }
 
 // ---- host side
@@ -711,6 +732,33 @@ hipError_t launch_one(const ConvMK2 &k2, size_t lds, hipStream_t st)
             if (e != hipSuccess) return e;
         }
         blocks = std::min<int64_t>(blocks, (int64_t)resident * g_n_cu);
+    }
+    static const int stag = [] {  // experiment knob: first-generation stagger units per resident slot
+        const char *e = getenv("MPCD_UNET_STAGGER");
+        return e ? atoi(e) : 0;
+    }();
+    if (!PERS && stag > 0) {
+        if (resident_lds != lds) {
+            int n = 0;
+            hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, MT, lds);
+            if (e != hipSuccess) return e;
+            resident = std::max(n, 1);
+            resident_lds = lds;
+        }
+        if (!g_n_cu) {
+            int dev = 0;
+            hipError_t e = hipGetDevice(&dev);
+            if (e == hipSuccess) e = hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+            if (e != hipSuccess) return e;
+        }
+        if (resident > 1 && blocks > (int64_t)resident * g_n_cu) {
+            ConvMK2 k3 = k2;
+            k3.ph[0].stag_units = stag;
+            k3.ph[0].stag_ncu = g_n_cu;
+            k3.ph[0].stag_slots = resident;
+            hipLaunchKernelGGL((conv_mx_kernel<KIND, P, NN, NC, PERS, NPH>), dim3((unsigned)blocks), dim3(MT), lds, st, k3);
+            return hipGetLastError();
+        }
     }
     hipLaunchKernelGGL((conv_mx_kernel<KIND, P, NN, NC, PERS, NPH>), dim3((unsigned)blocks), dim3(MT), lds, st, k2);
     return hipGetLastError();
@@ -1008,12 +1056,47 @@ hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::
            << pick.lds << ' ' << pick.stat_off;
         tune_cache_append(os.str());
     }
+    // diagnostics: MPCD_UNET_WGTRACE=<layer>[:<nth call>] records one launch's workgroup residency into
+    // gpurun_out/wgtrace_L<layer>.bin ({start, end, HW_ID, XCC_ID} per workgroup, s_memrealtime at 100 MHz)
+    static int tr_layer = -2, tr_call = 0;
+    if (tr_layer == -2) {
+        const char *e = getenv("MPCD_UNET_WGTRACE");
+        tr_layer = e && e[0] ? atoi(e) : -1;
+        const char *c = e ? strchr(e, ':') : nullptr;
+        tr_call = c ? atoi(c + 1) : 3;
+    }
+    if (tr_layer >= 0 && k.layer == tr_layer && --tr_call == 0) {
+        const int64_t nb = (k.rows + pick.rb - 1) / pick.rb;
+        uint32_t *dbuf = nullptr;
+        if (hipMalloc(&dbuf, (size_t)nb * 16) == hipSuccess) {
+            (void)hipMemsetAsync(dbuf, 0, (size_t)nb * 16, st);
+            ConvMK kk = k;
+            kk.skip = 0;
+            kk.wgtrace = dbuf;
+            hipError_t e = launch_choice(kind, planes, kk, pick, st);
+            std::vector<uint32_t> h((size_t)nb * 4);
+            if (e == hipSuccess && hipStreamSynchronize(st) == hipSuccess &&
+                hipMemcpy(h.data(), dbuf, (size_t)nb * 16, hipMemcpyDeviceToHost) == hipSuccess) {
+                char fn[128];
+                snprintf(fn, sizeof fn, "gpurun_out/wgtrace_L%d.bin", tr_layer);
+                if (FILE *f = fopen(fn, "wb")) {
+                    const int32_t hdr[4] = {(int32_t)nb, pick.rb, pick.t.nn * 16 + pick.t.nc, (int32_t)pick.lds};
+                    fwrite(hdr, 4, 4, f);
+                    fwrite(h.data(), 4, h.size(), f);
+                    fclose(f);
+                }
+            }
+            (void)hipFree(dbuf);
+            if (e != hipSuccess) return e;
+        }
+    }
     static const int skip = [] {  // experiment knob: skip kernel phases (results are garbage)
         const char *e = getenv("MPCD_UNET_SKIP");
         return e ? atoi(e) : 0;
     }();
     k.skip = skip;
-    if (skip) pick = cands[0].pers ? cands[1] : cands[0];
+    static const bool keep = getenv("MPCD_UNET_SKIP_KEEP") != nullptr;  // keep the tuned / cached pick
+    if (skip && (!keep || pick.pers)) pick = cands[0].pers ? cands[1] : cands[0];
     return launch_choice(kind, planes, k, pick, st);
 }
 

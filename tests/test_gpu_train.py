@@ -1,0 +1,109 @@
+"""the native training step (csrc/train.hip via mpcd_trainer_*) against the oracle's torch
+restatement (oracle/train.py: p_losses + WeightedL2 + autograd + torch.optim.Adam + EMA, fp32 CPU) on the same
+injected draws. Loss to 1e-5 relative; every gradient tensor to 1e-4 relative (norm); parameters after the Adam
+step to the Adam update's own resolution (elements whose gradient is tiny against the tensor's scale can flip
+the sign of lr*m/sqrt(v) on either side; those are counted, not compared)."""
+import numpy as np
+import pytest
+import torch
+
+from mpc_via_diffusion_model_amd import NetSpec
+from mpc_via_diffusion_model_amd.training import DiffusionTrainer
+from oracle import schedule as osch
+from oracle.train import OracleTrainer
+
+from ._util import make_mlp
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(d, H, C, B, N=100, seed=0, **kw):
+    net = make_mlp(d, H, C, seed=seed).train()
+    tables = osch.buffers("exponential", N)
+    tr = DiffusionTrainer(NetSpec("mlp", d, H, C), net.state_dict(), tables=tables, **kw)
+    orc = OracleTrainer(net, tables, **{k: v for k, v in kw.items() if k != "drop_prob"})
+    g = torch.Generator().manual_seed(seed + 1)
+    x0 = torch.rand(B, H, d, generator=g) * 2 - 1
+    ctx = torch.rand(B, C, generator=g) * 2 - 1
+    t, noise, mask = tr.draw(B, (B, H, d), generator=g)
+    return tr, orc, (x0, ctx, t, noise, mask)
+
+
+def _rel(a, b):
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("shape", [(2, 16, 4, 64), (2, 32, 4, 256), (1, 32, 2, 130)])
+def test_loss_matches_oracle(shape):
+    d, H, C, B = shape
+    tr, orc, batch = _setup(d, H, C, B)
+    with torch.no_grad():
+        ref = float(orc.loss(*batch))
+    got = tr.loss(*batch)
+    assert abs(got - ref) <= 1e-5 * abs(ref), (got, ref)
+
+
+@pytest.mark.parametrize("mask_kind", ["drawn", "all_dropped", "none_dropped"])
+def test_one_step_grads_params_ema(mask_kind):
+    d, H, C, B = 2, 32, 4, 192
+    tr, orc, (x0, ctx, t, noise, mask) = _setup(d, H, C, B, step_start_ema=1000, update_ema_every=10)
+    if mask_kind == "all_dropped":
+        mask = torch.ones_like(mask)
+    elif mask_kind == "none_dropped":
+        mask = torch.zeros_like(mask)
+    p0 = {k: v.clone() for k, v in orc.net.state_dict().items()}
+    ref_loss = orc.train_step(x0, ctx, t, noise, mask)
+    got_loss = tr.train_step(x0, ctx, t, noise, mask)
+    assert abs(got_loss - ref_loss) <= 1e-5 * abs(ref_loss)
+    grads = tr.state_dict("grads")
+    ref_grads = {n: p.grad for n, p in orc.net.named_parameters()}
+    for n, g in ref_grads.items():
+        if float(g.norm()) == 0.0:  # e.g. the context columns of every cond layer when all contexts are dropped
+            assert float(grads[n].norm()) == 0.0, n
+            continue
+        assert _rel(grads[n], g) <= 1e-4, (n, _rel(grads[n], g))
+    params = tr.state_dict("params")
+    ref_params = orc.net.state_dict()
+    lr = 3e-3
+    flipped = total = 0
+    for n, p in ref_params.items():
+        step_ref, step_got = p - p0[n], params[n] - p0[n]
+        g = ref_grads[n]
+        sure = g.abs() > 1e-3 * g.abs().max().clamp_min(1e-30)  # Adam's first step is ~lr*sign(g) there
+        assert torch.allclose(step_got[sure], step_ref[sure], rtol=1e-3, atol=1e-6 * lr), n
+        flipped += int((~torch.isclose(step_got, step_ref, rtol=1e-3, atol=1e-6 * lr) & ~sure).sum())
+        total += p.numel()
+    assert flipped <= 1e-3 * total, (flipped, total)
+    # step 0 < step_start_ema: the EMA model is reset to the model, then blended with it (trainer.py:302-308)
+    ema = tr.state_dict("ema")
+    for n, p in orc.ema.state_dict().items():
+        assert torch.allclose(ema[n], p, rtol=1e-3, atol=1e-6 * lr), n
+
+
+def test_twelve_steps_ema_blend_and_inference():
+    """12 steps with the EMA blend path live (step_start_ema=2, update every 5): losses track the oracle's and the
+    EMA weights load into the sampler."""
+    d, H, C, B = 2, 16, 4, 128
+    tr, orc, (x0, ctx, _, _, _) = _setup(d, H, C, B, step_start_ema=2, update_ema_every=5)
+    g = torch.Generator().manual_seed(7)
+    for s in range(12):
+        t, noise, mask = tr.draw(B, (B, H, d), generator=g)
+        ref = orc.train_step(x0, ctx, t, noise, mask)
+        got = tr.train_step(x0, ctx, t, noise, mask)
+        assert abs(got - ref) <= 2e-3 * abs(ref), (s, got, ref)
+    ema, ref_ema = tr.state_dict("ema"), orc.ema.state_dict()
+    assert max(_rel(ema[n], ref_ema[n]) for n in ref_ema) <= 1e-2
+    from mpc_via_diffusion_model_amd import DiffusionMPC
+    plan = DiffusionMPC(NetSpec("mlp", d, H, C), ema, n_diffusion_steps=100)
+    x = plan.sample_trajectories(ctx[:1], 32, H, seed=3)
+    assert x.shape == (32, H, d) and torch.isfinite(x).all()
+
+
+def test_rejects_bad_inputs():
+    tr, _, (x0, ctx, t, noise, mask) = _setup(2, 16, 4, 8)
+    with pytest.raises(ValueError):
+        tr.loss(x0, ctx, t + 1000, noise, mask)
+    with pytest.raises(ValueError):
+        tr.loss(x0, ctx[:, :3], t, noise, mask)
+    with pytest.raises(ValueError):
+        DiffusionTrainer(NetSpec("unet", 1, 32, 2), {}, n_diffusion_steps=10)
