@@ -169,7 +169,7 @@ __global__ void adam_kernel(int64_t n, float *p, const float *g, float *m, float
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const float gi = g[i];
         m[i] = m[i] + (1.f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1 - beta1)
-        v[i] = v[i] * b2 + (1.f - b2) * gi * gi;
+        v[i] = v[i] * b2 + (1.f - b2) * (gi * gi);  // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
         const float denom = sqrtf(v[i]) / bc2_sqrt + eps;
         p[i] = p[i] + (-step_size) * (m[i] / denom);
     }
