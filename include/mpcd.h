@@ -259,7 +259,8 @@ int mpcd_trainer_create(const mpcd_net_desc *desc, const float *params, size_t n
                         const float *sqrt_alphas_cumprod, const float *sqrt_one_minus_alphas_cumprod, int32_t n_steps,
                         mpcd_trainer **out);
 /* One batch (device pointers): x0 [B][H*d] normalised trajectories, context [B][C], t [B] (int64, < n_steps),
- * noise [B][H*d], context_mask [B] (1 = context dropped). update = 0: the loss only (p_losses forward);
+ * noise [B][H*d], context_mask [B] (1 = context dropped); t outside [0, n_steps) is clamped on the device (the
+ * Python wrapper rejects it). update = 0: the loss only (p_losses forward);
  * 1: loss, backward, Adam step, EMA update. Blocks until done; *loss = mean((eps_pred - noise)^2). */
 int mpcd_trainer_step(mpcd_trainer *tr, const float *x0, const float *context, const int64_t *t, const float *noise,
                       const float *context_mask, int64_t batch, int32_t update, double *loss, void *hip_stream);

@@ -97,11 +97,11 @@ __global__ void mish_bwd_kernel(int64_t n, const float *__restrict__ pre, const 
 
 // x_noisy = sqrt(abar_t) x0 + sqrt(1 - abar_t) noise  (q_sample, diffusion_model_base.py:421-431)
 __global__ void q_sample_kernel(int64_t B, int F, const float *x0, const float *noise, const int64_t *t,
-                                const float *sac, const float *s1mac, float *xn)
+                                const float *sac, const float *s1mac, int n_steps, float *xn)
 {
     const int64_t n = B * F;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t ti = t[i / F];
+        const int64_t ti = min(max(t[i / F], (int64_t)0), (int64_t)n_steps - 1);  // never read past the table
         const float u = sac[ti] * x0[i], v = s1mac[ti] * noise[i];
         xn[i] = u + v;
     }
@@ -335,7 +335,7 @@ struct Trainer {
         hipError_t e;
         // ---- forward (p_losses)
         hipLaunchKernelGGL(q_sample_kernel, dim3(grid_for(B * F)), dim3(256), 0, st, B, F, x0, noise, t, sched,
-                           sched + sp.n_steps, A.xn);
+                           sched + sp.n_steps, sp.n_steps, A.xn);
         hipLaunchKernelGGL(sinemb_kernel, dim3(grid_for(B * 32)), dim3(256), 0, st, B, t, A.e);
         if ((e = lin(B, A.e, 32, sp.t1, 0, 32, A.p1, 0.f, true)) != hipSuccess) return e;
         mish(B * 128, A.p1, A.q1);
