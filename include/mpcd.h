@@ -243,8 +243,8 @@ int mpcd_comm_init_loopback(mpcd_ctx *ctx, int32_t nranks, int32_t rank, uint64_
 
 /* ---- native training step: GaussianDiffusionModel.loss / p_losses with CFG context
  * dropout (diffusion_model_base.py:434-467), WeightedL2 (helpers.py:71-99), backward, torch.optim.Adam
- * (trainer.py:152) and the EMA model (trainer.py:70-88, 302-308), on the device in fp32. MLP noise-nets
- * (MPCD_NET_MLP) only. The random draws of p_losses (t ~ randint, noise ~ randn_like, context_mask ~
+ * (trainer.py:152) and the EMA model (trainer.py:70-88, 302-308), on the device in fp32. The CFG MLP net and
+ * ConditionedTemporalUnet (MPCD_NET_UNET with cfg_masked; training always runs in fp32 whatever desc->dtype). The random draws of p_losses (t ~ randint, noise ~ randn_like, context_mask ~
  * bernoulli(drop_prob)) are inputs, so a caller reproduces the reference's RNG stream exactly. */
 typedef struct mpcd_trainer mpcd_trainer;
 typedef struct {

@@ -1106,8 +1106,8 @@ int mpcd_trainer_create(const mpcd_net_desc *desc, const float *params, size_t n
     if (!out) return fail(MPCD_EINVAL, "null out");
     *out = nullptr;
     if (int r = check_desc(desc)) return r;
-    if (desc->kind != MPCD_NET_MLP || desc->dtype == MPCD_F16)
-        return fail(MPCD_EUNSUP, "mpcd_trainer: the CFG MLP noise-net in fp32 only");
+    if (desc->kind == MPCD_NET_UNET && !desc->cfg_masked)
+        return fail(MPCD_EUNSUP, "mpcd_trainer: the 3-arg TemporalUnet is not trainable here (ConditionedTemporalUnet is)");
     if (!params || !cfg || !sqrt_alphas_cumprod || !sqrt_one_minus_alphas_cumprod || n_steps < 1)
         return fail(MPCD_EINVAL, "mpcd_trainer_create: null argument or no schedule");
     const std::vector<PSpec> spec = param_spec(*desc);
@@ -1143,6 +1143,82 @@ int mpcd_trainer_create(const mpcd_net_desc *desc, const float *params, size_t n
     const int cond = cond_dim_of(*desc);
     sp.t1 = lin("time_mlp.encoder.1", 128, 32);
     sp.t2 = lin("time_mlp.encoder.3", desc->time_emb_dim, 128);
+    if (desc->kind == MPCD_NET_UNET) {  // ConditionedTemporalUnet trunk (temporal_unet.py:317-358) as an op tape
+        sp.unet = true;
+        const int H = desc->horizon, d = desc->state_dim, W = cond;
+        for (int i = 0; i + 1 < desc->n_mults; ++i)
+            if ((H >> (i + 1)) << (i + 1) != H) return fail(MPCD_EINVAL, "mpcd_trainer: horizon %d does not halve %d times", H, desc->n_mults - 1);
+        sp.ut = {UTensor{H, d}, UTensor{1, W}};
+        auto T = [&](int L, int C) {
+            sp.ut.push_back(UTensor{L, C});
+            return (int)sp.ut.size() - 1;
+        };
+        auto add_op = [&](int kind, int in0, int in1, int out, const std::string &pre, int k, int s_, int p_, int g) {
+            UOp o;
+            o.kind = kind;
+            o.in0 = in0;
+            o.in1 = in1;
+            o.out = out;
+            if (!pre.empty()) {
+                o.w = off.at(pre + ".weight");
+                o.b = off.at(pre + ".bias");
+            }
+            o.k = k;
+            o.s = s_;
+            o.p = p_;
+            o.groups = g;
+            sp.uops.push_back(o);
+            return out;
+        };
+        auto ngroups = [](int c) {
+            if (c < 8) return 1;
+            for (int g = 8; g < 18; ++g)
+                if (c % g == 0) return g;
+            return 1;
+        };
+        auto L_ = [&](int t) { return sp.ut[t].L; };
+        auto C_ = [&](int t) { return sp.ut[t].C; };
+        auto conv = [&](int x0, int x1, int Lo, int co, const std::string &pre, int k, int s_, int p_) {
+            return add_op(UOP_CONV, x0, x1, T(Lo, co), pre, k, s_, p_, 1);
+        };
+        auto gn = [&](int x, const std::string &pre) { return add_op(UOP_GN, x, -1, T(L_(x), C_(x)), pre, 1, 1, 0, ngroups(C_(x))); };
+        auto mish = [&](int x) { return add_op(UOP_MISH, x, -1, T(L_(x), C_(x)), "", 1, 1, 0, 1); };
+        auto rtb = [&](int x0, int x1, int co, const std::string &pre) {  // ResidualTemporalBlock (layers.py:323-355)
+            const int L = L_(x0), cin = C_(x0) + (x1 >= 0 ? C_(x1) : 0);
+            const int m1 = mish(gn(conv(x0, x1, L, co, pre + ".blocks.0.block.0", 5, 1, 2), pre + ".blocks.0.block.2"));
+            const int cc = add_op(UOP_LIN, UT_MC, -1, T(1, co), pre + ".cond_mlp.1", 1, 1, 0, 1);
+            const int h = add_op(UOP_ADDC, m1, cc, T(L, co), "", 1, 1, 0, 1);
+            const int m2 = mish(gn(conv(h, -1, L, co, pre + ".blocks.1.block.0", 5, 1, 2), pre + ".blocks.1.block.2"));
+            const int r = cin != co ? conv(x0, x1, L, co, pre + ".residual_conv", 1, 1, 0) : x0;
+            return add_op(UOP_ADD, m2, r, T(L, co), "", 1, 1, 0, 1);
+        };
+        auto st = stages(d, *desc);
+        const int nres = (int)st.size();
+        int x = UT_XNOISY;
+        std::vector<int> skips;
+        for (int i = 0; i < nres; ++i) {
+            const std::string p = "downs." + std::to_string(i);
+            x = rtb(x, -1, st[i].second, p + ".0");
+            x = rtb(x, -1, st[i].second, p + ".1");
+            skips.push_back(x);
+            if (i < nres - 1) x = conv(x, -1, L_(x) / 2, st[i].second, p + ".4.conv", 3, 2, 1);
+        }
+        x = rtb(x, -1, st.back().second, "mid_block1");
+        x = rtb(x, -1, st.back().second, "mid_block2");
+        for (int i = 1; i < nres; ++i) {
+            const int ci = st[nres - i].first;
+            const std::string p = "ups." + std::to_string(i - 1);
+            const int skip = skips.back();
+            skips.pop_back();
+            x = rtb(x, skip, ci, p + ".0");
+            x = rtb(x, -1, ci, p + ".1");
+            x = add_op(UOP_CONVT, x, -1, T(2 * L_(x), ci), p + ".4.conv", 4, 2, 1, 1);
+        }
+        x = mish(gn(conv(x, -1, H, desc->base_dim, "final_conv.0.block.0", 5, 1, 2), "final_conv.0.block.2"));
+        sp.u_out = add_op(UOP_LIN, x, -1, T(H, d), "final_conv.1", 1, 1, 0, 1);
+        if (L_(sp.u_out) != H) return fail(MPCD_EINVAL, "mpcd_trainer: U-Net tape ends at %d positions, not %d", L_(sp.u_out), H);
+        (void)W;
+    }
     auto st = stages(sp.flat, *desc);
     const int ns = (int)st.size();
     auto block = [&](const std::string &p, int ci, int co, int in0, int in1) {
@@ -1155,14 +1231,17 @@ int mpcd_trainer_create(const mpcd_net_desc *desc, const float *params, size_t n
         b.in1 = in1;
         return b;
     };
-    for (int i = 0; i < ns; ++i) sp.blocks.push_back(block("downs." + std::to_string(i) + ".0", st[i].first, st[i].second, i - 1, -1));
-    sp.blocks.push_back(block("mid_block1", st.back().second, st.back().second, ns - 1, -1));
-    for (int i = 1; i < ns; ++i) {  // ups.{i-1}: cat(previous output, skip = downs.{ns-i})
+    for (int i = 0; i < ns && !sp.unet; ++i)
+        sp.blocks.push_back(block("downs." + std::to_string(i) + ".0", st[i].first, st[i].second, i - 1, -1));
+    if (!sp.unet) sp.blocks.push_back(block("mid_block1", st.back().second, st.back().second, ns - 1, -1));
+    for (int i = 1; i < ns && !sp.unet; ++i) {  // ups.{i-1}: cat(previous output, skip = downs.{ns-i})
         auto [ci, co] = st[ns - i];
         sp.blocks.push_back(block("ups." + std::to_string(i - 1) + ".0", 2 * co, ci, (int)sp.blocks.size() - 1, ns - i));
     }
-    sp.f1 = lin("final_layer.0._network.0", desc->base_dim, desc->base_dim);
-    sp.f2 = lin("final_layer.0._network.2", sp.flat, desc->base_dim);
+    if (!sp.unet) {
+        sp.f1 = lin("final_layer.0._network.0", desc->base_dim, desc->base_dim);
+        sp.f2 = lin("final_layer.0._network.2", sp.flat, desc->base_dim);
+    }
     std::vector<float> sched((size_t)2 * n_steps);
     std::copy(sqrt_alphas_cumprod, sqrt_alphas_cumprod + n_steps, sched.begin());
     std::copy(sqrt_one_minus_alphas_cumprod, sqrt_one_minus_alphas_cumprod + n_steps, sched.begin() + n_steps);

@@ -84,15 +84,217 @@ __global__ void mish_fwd_kernel(int64_t n, const float *__restrict__ pre, float 
         out[i] = pre[i] * tanhf(softplus(pre[i]));
 }
 
-// d pre = d out * (tanh(sp) + x * sigmoid(x) * (1 - tanh(sp)^2))  (torch's Mish backward); in place allowed
-__global__ void mish_bwd_kernel(int64_t n, const float *__restrict__ pre, const float *dout, float *dpre)
+// d pre (+)= d out * (tanh(sp) + x * sigmoid(x) * (1 - tanh(sp)^2))  (torch's Mish backward); in place allowed
+__global__ void mish_bwd_kernel(int64_t n, const float *__restrict__ pre, const float *dout, float *dpre, int acc)
 {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const float x = pre[i];
         const float tsp = tanhf(softplus(x));
         const float sg = 1.f / (1.f + expf(-x));
-        dpre[i] = dout[i] * (tsp + x * sg * (1.f - tsp * tsp));
+        const float d = dout[i] * (tsp + x * sg * (1.f - tsp * tsp));
+        dpre[i] = acc ? dpre[i] + d : d;
     }
+}
+
+// ---- U-Net trunk ops, channels-last [b][l][c]
+
+// col[(b*Lout + o)][ci*k + tap] = x(b, o*s - p + tap, ci), ci < ca from xa, else from xb (channel concat)
+__global__ void im2col_kernel(int64_t B, int Lin, int Lout, int ca, int cb, int k, int s, int p, const float *xa,
+                              const float *xb, float *col)
+{
+    const int cin = ca + cb, W = cin * k;
+    const int64_t n = B * Lout * W;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / W;
+        const int j = (int)(i - r * W), ci = j / k, tap = j - ci * k;
+        const int64_t b = r / Lout;
+        const int o = (int)(r - b * Lout), pos = o * s - p + tap;
+        float v = 0.f;
+        if (pos >= 0 && pos < Lin)
+            v = ci < ca ? xa[(b * Lin + pos) * ca + ci] : xb[(b * Lin + pos) * cb + (ci - ca)];
+        col[i] = v;
+    }
+}
+
+// dx(b, i, ci) += sum over (o, tap) with o*s - p + tap = i of dcol[(b*Lout + o)][ci*k + tap]  (gather, no atomics)
+__global__ void col2im_kernel(int64_t B, int Lin, int Lout, int ca, int cb, int k, int s, int p, const float *dcol,
+                              float *dxa, float *dxb)
+{
+    const int cin = ca + cb, W = cin * k;
+    const int64_t n = B * Lin * cin;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / cin;
+        const int ci = (int)(i - r * cin);
+        const int64_t b = r / Lin;
+        const int pos = (int)(r - b * Lin);
+        float acc = 0.f;
+        for (int tap = 0; tap < k; ++tap) {
+            const int q = pos + p - tap;
+            if (q < 0 || q % s) continue;
+            const int o = q / s;
+            if (o >= Lout) continue;
+            acc += dcol[(b * Lout + o) * W + ci * k + tap];
+        }
+        if (ci < ca) {
+            if (dxa) dxa[(b * Lin + pos) * ca + ci] += acc;
+        } else if (dxb) {
+            dxb[(b * Lin + pos) * cb + (ci - ca)] += acc;
+        }
+    }
+}
+
+// ConvTranspose1d: y(b, o, co) = bias[co] + sum over (i, tap) with i*s - p + tap = o of ycol[(b*Lin + i)][co*k + tap]
+__global__ void convt_gather_kernel(int64_t B, int Lin, int Lout, int C, int k, int s, int p, const float *ycol,
+                                    const float *bias, float *y)
+{
+    const int64_t n = B * Lout * C;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / C;
+        const int co = (int)(i - r * C);
+        const int64_t b = r / Lout;
+        const int o = (int)(r - b * Lout);
+        float acc = 0.f;
+        for (int tap = 0; tap < k; ++tap) {
+            const int q = o + p - tap;
+            if (q < 0 || q % s) continue;
+            const int ii = q / s;
+            if (ii >= Lin) continue;
+            acc += ycol[(b * Lin + ii) * (C * k) + co * k + tap];
+        }
+        y[i] = acc + bias[co];
+    }
+}
+
+// dycol[(b*Lin + i)][co*k + tap] = dy(b, i*s - p + tap, co) (0 outside)
+__global__ void convt_scatter_kernel(int64_t B, int Lin, int Lout, int C, int k, int s, int p, const float *dy,
+                                     float *dycol)
+{
+    const int W = C * k;
+    const int64_t n = B * Lin * W;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / W;
+        const int j = (int)(i - r * W), co = j / k, tap = j - co * k;
+        const int64_t b = r / Lin;
+        const int ii = (int)(r - b * Lin), o = ii * s - p + tap;
+        dycol[i] = (o >= 0 && o < Lout) ? dy[(b * Lout + o) * C + co] : 0.f;
+    }
+}
+
+// GroupNorm over (L positions x C/G channels) per (row, group), eps 1e-5: one workgroup per (b, g)
+__global__ __launch_bounds__(256) void gn_fwd_kernel(int L, int C, int G, const float *x, const float *w, const float *bb,
+                                                     float *y, float *stat)
+{
+    __shared__ double s1[256], s2[256];
+    const int64_t b = blockIdx.x / G;
+    const int g = blockIdx.x % G, cpg = C / G, n = L * cpg;
+    const float *xb = x + b * L * C + g * cpg;
+    double a1 = 0, a2 = 0;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const double v = xb[(i / cpg) * C + i % cpg];
+        a1 += v;
+        a2 += v * v;
+    }
+    s1[threadIdx.x] = a1;
+    s2[threadIdx.x] = a2;
+    __syncthreads();
+    for (int m = 128; m > 0; m >>= 1) {
+        if ((int)threadIdx.x < m) {
+            s1[threadIdx.x] += s1[threadIdx.x + m];
+            s2[threadIdx.x] += s2[threadIdx.x + m];
+        }
+        __syncthreads();
+    }
+    const double mean = s1[0] / n, var = fmax(s2[0] / n - mean * mean, 0.0);
+    const float mf = (float)mean, rs = (float)(1.0 / sqrt(var + 1e-5));
+    if (threadIdx.x == 0) {
+        stat[2 * blockIdx.x] = mf;
+        stat[2 * blockIdx.x + 1] = rs;
+    }
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const int l = i / cpg, c = g * cpg + i % cpg;
+        const int64_t e = (b * L + l) * C + c;
+        y[e] = (x[e] - mf) * rs * w[c] + bb[c];
+    }
+}
+
+// GroupNorm backward: dx += rstd * (dxh - mean(dxh) - xh * mean(dxh * xh)), dxh = dy * w; per-row partials of
+// d weight (dy * xh) and d bias (dy) into part[b][2][C] (reduced over rows by colsum afterwards)
+__global__ __launch_bounds__(256) void gn_bwd_kernel(int L, int C, int G, const float *x, const float *dy, const float *w,
+                                                     const float *stat, float *dx, float *part)
+{
+    __shared__ double s1[256], s2[256];
+    const int64_t b = blockIdx.x / G;
+    const int g = blockIdx.x % G, cpg = C / G, n = L * cpg;
+    const float mf = stat[2 * blockIdx.x], rs = stat[2 * blockIdx.x + 1];
+    double a1 = 0, a2 = 0;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const int l = i / cpg, c = g * cpg + i % cpg;
+        const int64_t e = (b * L + l) * C + c;
+        const float xh = (x[e] - mf) * rs, d = dy[e] * w[c];
+        a1 += d;
+        a2 += (double)d * xh;
+    }
+    s1[threadIdx.x] = a1;
+    s2[threadIdx.x] = a2;
+    __syncthreads();
+    for (int m = 128; m > 0; m >>= 1) {
+        if ((int)threadIdx.x < m) {
+            s1[threadIdx.x] += s1[threadIdx.x + m];
+            s2[threadIdx.x] += s2[threadIdx.x + m];
+        }
+        __syncthreads();
+    }
+    const float m1 = (float)(s1[0] / n), m2 = (float)(s2[0] / n);
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const int l = i / cpg, c = g * cpg + i % cpg;
+        const int64_t e = (b * L + l) * C + c;
+        const float xh = (x[e] - mf) * rs, d = dy[e] * w[c];
+        dx[e] += rs * (d - m1 - xh * m2);
+    }
+    // affine partials: one thread per channel of the group, over the positions
+    for (int cc = threadIdx.x; cc < cpg; cc += 256) {
+        const int c = g * cpg + cc;
+        float gw = 0.f, gb = 0.f;
+        for (int l = 0; l < L; ++l) {
+            const int64_t e = (b * L + l) * C + c;
+            gw += dy[e] * ((x[e] - mf) * rs);
+            gb += dy[e];
+        }
+        part[b * 2 * C + c] = gw;
+        part[b * 2 * C + C + c] = gb;
+    }
+}
+
+// y[b][l][c] = x[b][l][c] + cond[b][c]
+__global__ void addc_kernel(int64_t B, int L, int C, const float *x, const float *cond, float *y)
+{
+    const int64_t n = B * L * C;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = x[i] + cond[(i / ((int64_t)L * C)) * C + i % C];
+}
+
+// dcond[b][c] += sum_l dy[b][l][c]
+__global__ void rowsum_l_kernel(int64_t B, int L, int C, const float *dy, float *dcond)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < B * C; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = i / C;
+        const int c = (int)(i - b * C);
+        float acc = 0.f;
+        for (int l = 0; l < L; ++l) acc += dy[(b * L + l) * C + c];
+        dcond[i] += acc;
+    }
+}
+
+__global__ void add_kernel(int64_t n, const float *a, const float *b, float *y)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = a[i] + b[i];
+}
+
+__global__ void acc_kernel(int64_t n, const float *d, float *g)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        g[i] += d[i];
 }
 
 // x_noisy = sqrt(abar_t) x0 + sqrt(1 - abar_t) noise  (q_sample, diffusion_model_base.py:421-431)
@@ -239,9 +441,151 @@ struct Trainer {
     {
         hipLaunchKernelGGL(mish_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, pre, out);
     }
-    void mish_bwd(int64_t n, const float *pre, const float *dout, float *dpre)
+    void mish_bwd(int64_t n, const float *pre, const float *dout, float *dpre, int acc = 0)
     {
-        hipLaunchKernelGGL(mish_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, pre, dout, dpre);
+        hipLaunchKernelGGL(mish_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, pre, dout, dpre, acc);
+    }
+
+    // ---- U-Net trunk tape: per tensor value / gradient, per op scratch (im2col, GroupNorm statistics)
+    struct UBuf {
+        float *v = nullptr, *g = nullptr;
+    };
+    std::vector<UBuf> U;
+    std::vector<float *> ucol, ustat, upart;
+    int tL(int t) const { return sp.ut[t].L; }
+    int tC(int t) const { return sp.ut[t].C; }
+
+    int reserve_unet(int64_t B)
+    {
+        const int nt = (int)sp.ut.size(), no = (int)sp.uops.size();
+        U.assign(nt, UBuf{});
+        U[UT_XNOISY] = {A.xn, nullptr};
+        U[UT_MC] = {A.mc, A.dmc};
+        for (int t = 2; t < nt; ++t) {
+            if (t == sp.u_out) {
+                U[t] = {A.out, A.dout};
+                continue;
+            }
+            U[t].v = alloc(B * tL(t) * tC(t));
+            U[t].g = alloc(B * tL(t) * tC(t));
+        }
+        ucol.assign(no, nullptr);
+        ustat = upart = ucol;
+        for (int i = 0; i < no; ++i) {
+            const UOp &o = sp.uops[i];
+            if (o.kind == UOP_CONV) {
+                const int cin = tC(o.in0) + (o.in1 >= 0 ? tC(o.in1) : 0);
+                ucol[i] = alloc(B * tL(o.out) * cin * o.k);
+            } else if (o.kind == UOP_CONVT) {
+                ucol[i] = alloc(B * tL(o.in0) * tC(o.out) * o.k);
+            } else if (o.kind == UOP_GN) {
+                ustat[i] = alloc(2 * B * o.groups);
+                upart[i] = alloc(2 * B * tC(o.out));
+            }
+        }
+        return 0;
+    }
+
+    hipError_t unet_fwd(int64_t B)
+    {
+        hipError_t e = hipSuccess;
+        for (size_t i = 0; i < sp.uops.size() && e == hipSuccess; ++i) {
+            const UOp &o = sp.uops[i];
+            const float *x0 = U[o.in0].v, *x1 = o.in1 >= 0 ? U[o.in1].v : nullptr;
+            float *y = U[o.out].v;
+            const int Li = tL(o.in0), Lo = tL(o.out), Ci = tC(o.in0), Co = tC(o.out);
+            switch (o.kind) {
+            case UOP_CONV: {
+                const int cb = o.in1 >= 0 ? tC(o.in1) : 0, K = (Ci + cb) * o.k;
+                hipLaunchKernelGGL(im2col_kernel, dim3(grid_for(B * Lo * K)), dim3(256), 0, st, B, Li, Lo, Ci, cb, o.k,
+                                   o.s, o.p, x0, x1, ucol[i]);
+                e = gemm((int)(B * Lo), Co, K, ucol[i], K, 1, P + o.w, 1, K, y, Co, 0.f, P + o.b);
+                break;
+            }
+            case UOP_CONVT: {
+                const int K = Co * o.k;
+                e = gemm((int)(B * Li), K, Ci, x0, Ci, 1, P + o.w, K, 1, ucol[i], K, 0.f, nullptr);
+                hipLaunchKernelGGL(convt_gather_kernel, dim3(grid_for(B * Lo * Co)), dim3(256), 0, st, B, Li, Lo, Co,
+                                   o.k, o.s, o.p, ucol[i], P + o.b, y);
+                break;
+            }
+            case UOP_GN:
+                hipLaunchKernelGGL(gn_fwd_kernel, dim3((unsigned)(B * o.groups)), dim3(256), 0, st, Li, Ci, o.groups, x0,
+                                   P + o.w, P + o.b, y, ustat[i]);
+                break;
+            case UOP_MISH: mish(B * Li * Ci, x0, y); break;
+            case UOP_ADDC:
+                hipLaunchKernelGGL(addc_kernel, dim3(grid_for(B * Li * Ci)), dim3(256), 0, st, B, Li, Ci, x0, x1, y);
+                break;
+            case UOP_ADD:
+                hipLaunchKernelGGL(add_kernel, dim3(grid_for(B * Li * Ci)), dim3(256), 0, st, B * Li * Ci, x0, x1, y);
+                break;
+            case UOP_LIN: e = gemm((int)(B * Li), Co, Ci, x0, Ci, 1, P + o.w, 1, Ci, y, Co, 0.f, P + o.b); break;
+            }
+            if (e == hipSuccess) e = hipGetLastError();
+        }
+        return e;
+    }
+
+    hipError_t unet_bwd(int64_t B)
+    {
+        hipError_t e = hipSuccess;
+        for (int i = (int)sp.uops.size() - 1; i >= 0 && e == hipSuccess; --i) {
+            const UOp &o = sp.uops[i];
+            const float *x0 = U[o.in0].v, *go = U[o.out].g;
+            float *g0 = U[o.in0].g, *g1 = o.in1 >= 0 ? U[o.in1].g : nullptr;
+            const int Li = tL(o.in0), Lo = tL(o.out), Ci = tC(o.in0), Co = tC(o.out);
+            switch (o.kind) {
+            case UOP_CONV: {
+                const int cb = o.in1 >= 0 ? tC(o.in1) : 0, K = (Ci + cb) * o.k;
+                const int64_t R = B * Lo;
+                hipLaunchKernelGGL(colsum_kernel, dim3((Co + 63) / 64), dim3(256), 0, st, R, Co, go, (int64_t)Co, G + o.b);
+                e = gemm(Co, K, (int)R, go, 1, Co, ucol[i], K, 1, G + o.w, K, 1.f, nullptr);
+                if (e == hipSuccess && (g0 || g1)) {
+                    e = gemm((int)R, K, Co, go, Co, 1, P + o.w, K, 1, ucol[i], K, 0.f, nullptr);
+                    hipLaunchKernelGGL(col2im_kernel, dim3(grid_for(B * Li * (Ci + cb))), dim3(256), 0, st, B, Li, Lo, Ci,
+                                       cb, o.k, o.s, o.p, ucol[i], g0, g1);
+                }
+                break;
+            }
+            case UOP_CONVT: {
+                const int K = Co * o.k;
+                hipLaunchKernelGGL(convt_scatter_kernel, dim3(grid_for(B * Li * K)), dim3(256), 0, st, B, Li, Lo, Co, o.k,
+                                   o.s, o.p, go, ucol[i]);
+                e = gemm(Ci, K, (int)(B * Li), x0, 1, Ci, ucol[i], K, 1, G + o.w, K, 1.f, nullptr);
+                hipLaunchKernelGGL(colsum_kernel, dim3((Co + 63) / 64), dim3(256), 0, st, B * Lo, Co, go, (int64_t)Co,
+                                   G + o.b);
+                if (e == hipSuccess && g0) e = gemm((int)(B * Li), Ci, K, ucol[i], K, 1, P + o.w, 1, K, g0, Ci, 1.f, nullptr);
+                break;
+            }
+            case UOP_GN:
+                hipLaunchKernelGGL(gn_bwd_kernel, dim3((unsigned)(B * o.groups)), dim3(256), 0, st, Li, Ci, o.groups, x0, go,
+                                   P + o.w, ustat[i], g0, upart[i]);
+                hipLaunchKernelGGL(colsum_kernel, dim3((Ci + 63) / 64), dim3(256), 0, st, B, Ci, upart[i], (int64_t)2 * Ci,
+                                   G + o.w);
+                hipLaunchKernelGGL(colsum_kernel, dim3((Ci + 63) / 64), dim3(256), 0, st, B, Ci, upart[i] + Ci,
+                                   (int64_t)2 * Ci, G + o.b);
+                break;
+            case UOP_MISH: mish_bwd(B * Li * Ci, x0, go, g0, 1); break;
+            case UOP_ADDC:
+                hipLaunchKernelGGL(acc_kernel, dim3(grid_for(B * Li * Ci)), dim3(256), 0, st, B * Li * Ci, go, g0);
+                hipLaunchKernelGGL(rowsum_l_kernel, dim3(grid_for(B * Ci)), dim3(256), 0, st, B, Li, Ci, go, g1);
+                break;
+            case UOP_ADD:
+                hipLaunchKernelGGL(acc_kernel, dim3(grid_for(B * Li * Ci)), dim3(256), 0, st, B * Li * Ci, go, g0);
+                hipLaunchKernelGGL(acc_kernel, dim3(grid_for(B * Li * Ci)), dim3(256), 0, st, B * Li * Ci, go, g1);
+                break;
+            case UOP_LIN: {
+                const int64_t R = B * Li;
+                hipLaunchKernelGGL(colsum_kernel, dim3((Co + 63) / 64), dim3(256), 0, st, R, Co, go, (int64_t)Co, G + o.b);
+                e = gemm(Co, Ci, (int)R, go, 1, Co, x0, Ci, 1, G + o.w, Ci, 1.f, nullptr);
+                if (e == hipSuccess && g0) e = gemm((int)R, Ci, Co, go, Co, 1, P + o.w, Ci, 1, g0, Ci, 1.f, nullptr);
+                break;
+            }
+            }
+            if (e == hipSuccess) e = hipGetLastError();
+        }
+        return e;
     }
 
     // activation buffers per training row count
@@ -281,6 +625,7 @@ struct Trainer {
             A.dy[j] = alloc(B * co);
             A.dh[j] = alloc(B * co);
         }
+        if (sp.unet) reserve_unet(B);
         for (float *b : bufs)
             if (!b) return -1;
         cap = B;
@@ -342,11 +687,15 @@ struct Trainer {
         if ((e = lin(B, A.q1, 128, sp.t2, 0, 128, A.temb, 0.f, true)) != hipSuccess) return e;
         hipLaunchKernelGGL(cemb_kernel, dim3(grid_for(B * W)), dim3(256), 0, st, B, T, C, A.temb, ctx, mask, A.cemb);
         mish(B * W, A.cemb, A.mc);
-        for (int j = 0; j < nb; ++j)
-            if ((e = block_fwd(B, j)) != hipSuccess) return e;
         const int last = nb - 1;
-        if ((e = lin(B, A.y[last], sp.base, sp.f1, 0, sp.base, A.f1, 0.f, true)) != hipSuccess) return e;
-        if ((e = lin(B, A.f1, sp.base, sp.f2, 0, sp.base, A.out, 0.f, true)) != hipSuccess) return e;
+        if (sp.unet) {
+            if ((e = unet_fwd(B)) != hipSuccess) return e;
+        } else {
+            for (int j = 0; j < nb; ++j)
+                if ((e = block_fwd(B, j)) != hipSuccess) return e;
+            if ((e = lin(B, A.y[last], sp.base, sp.f1, 0, sp.base, A.f1, 0.f, true)) != hipSuccess) return e;
+            if ((e = lin(B, A.f1, sp.base, sp.f2, 0, sp.base, A.out, 0.f, true)) != hipSuccess) return e;
+        }
         // ---- loss = mean((eps - noise)^2)  (WeightedL2, predict_epsilon)
         const int64_t n = B * F;
         const unsigned nbk = std::min<unsigned>(grid_for(n), 1024);
@@ -367,12 +716,19 @@ struct Trainer {
         for (int j = 0; j < nb; ++j)
             if ((e = hipMemsetAsync(A.dy[j], 0, (size_t)B * sp.blocks[j].co * 4, st)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(A.dmc, 0, (size_t)B * W * 4, st)) != hipSuccess) return e;
-        if ((e = bias_bwd(B, sp.f2, A.dout)) != hipSuccess) return e;
-        if ((e = lin_bwd(B, A.f1, sp.base, sp.f2, 0, sp.base, A.dout, A.tmp, 0.f)) != hipSuccess) return e;  // d f1
-        if ((e = bias_bwd(B, sp.f1, A.tmp)) != hipSuccess) return e;
-        if ((e = lin_bwd(B, A.y[last], sp.base, sp.f1, 0, sp.base, A.tmp, A.dy[last], 1.f)) != hipSuccess) return e;
-        for (int j = nb - 1; j >= 0; --j)
-            if ((e = block_bwd(B, j)) != hipSuccess) return e;
+        if (sp.unet) {
+            for (int t = 2; t < (int)U.size(); ++t)
+                if (t != sp.u_out && (e = hipMemsetAsync(U[t].g, 0, (size_t)B * tL(t) * tC(t) * 4, st)) != hipSuccess)
+                    return e;
+            if ((e = unet_bwd(B)) != hipSuccess) return e;
+        } else {
+            if ((e = bias_bwd(B, sp.f2, A.dout)) != hipSuccess) return e;
+            if ((e = lin_bwd(B, A.f1, sp.base, sp.f2, 0, sp.base, A.dout, A.tmp, 0.f)) != hipSuccess) return e;  // d f1
+            if ((e = bias_bwd(B, sp.f1, A.tmp)) != hipSuccess) return e;
+            if ((e = lin_bwd(B, A.y[last], sp.base, sp.f1, 0, sp.base, A.tmp, A.dy[last], 1.f)) != hipSuccess) return e;
+            for (int j = nb - 1; j >= 0; --j)
+                if ((e = block_bwd(B, j)) != hipSuccess) return e;
+        }
         mish_bwd(B * W, A.cemb, A.dmc, A.dcemb);
         // time MLP: d t_emb = d c_emb[:, :T] (row stride W)
         if ((e = gemm(sp.t2.n, 128, (int)B, A.dcemb, 1, W, A.q1, 128, 1, G + sp.t2.w, 128, 1.f, nullptr)) != hipSuccess) return e;

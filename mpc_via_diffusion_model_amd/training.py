@@ -1,4 +1,4 @@
-"""Native training step for the CFG MLP noise-net behind the reference's interface:
+"""Native training step for the CFG MLP noise-net and ConditionedTemporalUnet behind the reference's interface:
 GaussianDiffusionModel.loss(x, context) -> p_losses (mpd/models/diffusion_models/diffusion_model_base.py:
 434-472) with CFG context dropout (drop_prob, :57, :449), the WeightedL2 loss (helpers.py:71-99), and the
 trainer's optimisation step (mpd/trainer/trainer.py:152 Adam, :284-308 backward / step / EMA).
@@ -20,10 +20,10 @@ class DiffusionTrainer:
     def __init__(self, spec, params, variance_schedule="exponential", n_diffusion_steps=100, tables=None, lr=3e-3,
                  betas=(0.9, 0.999), eps=1e-8, ema_decay=0.995, step_start_ema=1000, update_ema_every=10,
                  drop_prob=0.25, device=None):
-        """spec: NetSpec(kind="mlp", ...); params: state_dict of the net (no "model." prefix). Defaults are the
+        """spec: NetSpec(kind="mlp" or "unet" with cfg=True, ...); params: state_dict of the net (no "model." prefix). Defaults are the
         reference's (NN_cart_pole_train.py:143,168-170; diffusion_model_base.py:57; torch Adam)."""
-        if spec.kind != "mlp":
-            raise ValueError("the native training step covers the MLP noise-net")
+        if spec.kind not in ("mlp", "unet") or (spec.kind == "unet" and not spec.cfg):
+            raise ValueError("the native training step covers the CFG MLP noise-net and ConditionedTemporalUnet")
         self.spec = spec
         self.drop_prob = float(drop_prob)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
