@@ -187,7 +187,7 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
     extern __shared__ __attribute__((aligned(16))) char sm[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    const uint32_t t_start = as.ph[0].wgtrace ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
     if constexpr (!PERS) {
         const ConvMK &a0 = as.ph[0];
         if (a0.stag_units > 0 && (int64_t)blockIdx.x < (int64_t)a0.stag_ncu * a0.stag_slots) {
