@@ -27,21 +27,25 @@ constexpr int GK = 16;   // k-step staged in LDS
 
 // C[m][n] (ldc) = beta * C + sum_k A(m,k) B(k,n) (+ bias[n]); A(m,k) = a[m*sam + k*sak], B(k,n) = b[k*sbk + n*sbn].
 // 256 threads, each a 4x4 block of C; the k-sum runs in k order per output (fp32 FMA off: -ffp-contract=off).
+// Split K (gridDim.z > 1): slice z sums k in [z*kchunk, (z+1)*kchunk) into c + z*zstride (beta 0, no bias);
+// splitk_reduce_kernel then adds the slices in z order (deterministic).
 __global__ __launch_bounds__(256) void gemm_kernel(int M, int N, int K, const float *__restrict__ a, int64_t sam,
                                                    int64_t sak, const float *__restrict__ b, int64_t sbk, int64_t sbn,
                                                    float *__restrict__ c, int64_t ldc, float beta,
-                                                   const float *__restrict__ bias)
+                                                   const float *__restrict__ bias, int kchunk, int64_t zstride)
 {
     __shared__ float As[GK][GT + 1], Bs[GK][GT + 1];
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
+    const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
+    c += blockIdx.z * zstride;
     float acc[4][4] = {};
-    for (int k0 = 0; k0 < K; k0 += GK) {
+    for (int k0 = kb; k0 < ke; k0 += GK) {
         for (int i = threadIdx.x; i < GK * GT; i += 256) {
             const int kk = i / GT, r = i % GT;
             const int m = m0 + r, n = n0 + r, k = k0 + kk;
-            As[kk][r] = (m < M && k < K) ? a[m * sam + k * sak] : 0.f;
-            Bs[kk][r] = (n < N && k < K) ? b[k * sbk + n * sbn] : 0.f;
+            As[kk][r] = (m < M && k < ke) ? a[m * sam + k * sak] : 0.f;
+            Bs[kk][r] = (n < N && k < ke) ? b[k * sbk + n * sbn] : 0.f;
         }
         __syncthreads();
 #pragma unroll
@@ -73,6 +77,46 @@ __global__ __launch_bounds__(256) void gemm_kernel(int M, int N, int K, const fl
             *p = beta != 0.f ? *p + v : v;
         }
     }
+}
+
+// C[m][n] = beta * C + sum_z part[z][m][n] (+ bias[n])
+__global__ void splitk_reduce_kernel(int M, int N, int Z, const float *part, float *c, int64_t ldc, float beta,
+                                     const float *bias)
+{
+    const int64_t n = (int64_t)M * N;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        float acc = 0.f;
+        for (int z = 0; z < Z; ++z) acc += part[z * n + i];
+        const int m = (int)(i / N), j = (int)(i - (int64_t)m * N);
+        if (bias) acc += bias[j];
+        float *p = c + m * ldc + j;
+        *p = beta != 0.f ? *p + acc : acc;
+    }
+}
+
+// column sums over a row slice: part[z][n] = sum_{m in slice z} dy[m*ld + n]
+__global__ __launch_bounds__(256) void colsum_part_kernel(int64_t M, int N, const float *dy, int64_t ld, int64_t rchunk,
+                                                          float *part)
+{
+    __shared__ float s[4][64];
+    const int c = threadIdx.x & 63, r = threadIdx.x >> 6, n = blockIdx.x * 64 + c;
+    const int64_t mb = blockIdx.y * rchunk, me = min(M, mb + rchunk);
+    float acc = 0.f;
+    if (n < N)
+        for (int64_t m = mb + r; m < me; m += 4) acc += dy[m * ld + n];
+    s[r][c] = acc;
+    __syncthreads();
+    if (r == 0 && n < N) part[blockIdx.y * (int64_t)N + n] = (s[0][c] + s[1][c]) + (s[2][c] + s[3][c]);
+}
+
+// db[n] += sum_z part[z][n]
+__global__ void colsum_reduce_kernel(int N, int Z, const float *part, float *db)
+{
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    float acc = 0.f;
+    for (int z = 0; z < Z; ++z) acc += part[(int64_t)z * N + n];
+    db[n] += acc;
 }
 
 MPCD_DEV float softplus(float x) { return log1pf(expf(x)); }  // as torch's Mish kernels (no threshold)
@@ -402,7 +446,7 @@ struct Trainer {
     ~Trainer()
     {
         for (float *b : bufs) (void)hipFree(b);
-        for (float *b : {P, G, Mo, Vo, E, sched}) (void)hipFree(b);
+        for (float *b : {P, G, Mo, Vo, E, sched, ws}) (void)hipFree(b);
         (void)hipFree(part);
     }
     float *alloc(int64_t n)
@@ -412,11 +456,56 @@ struct Trainer {
         bufs.push_back(p);
         return p;
     }
+    // split-K / split-row workspace (grown on demand; the stream orders its reuse)
+    float *ws = nullptr;
+    int64_t ws_n = 0;
+    float *workspace(int64_t n)
+    {
+        if (n > ws_n) {
+            (void)hipStreamSynchronize(st);
+            (void)hipFree(ws);
+            ws = nullptr;
+            ws_n = 0;
+            if (hipMalloc(&ws, (size_t)n * 4) != hipSuccess) return nullptr;
+            ws_n = n;
+        }
+        return ws;
+    }
     hipError_t gemm(int M, int N, int K, const float *a, int64_t sam, int64_t sak, const float *b, int64_t sbk,
                     int64_t sbn, float *c, int64_t ldc, float beta, const float *bias)
     {
         dim3 g((N + GT - 1) / GT, (M + GT - 1) / GT);
-        hipLaunchKernelGGL(gemm_kernel, g, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, c, ldc, beta, bias);
+        const int64_t tiles = (int64_t)g.x * g.y;
+        // the weight-gradient GEMMs (M, N <= a few hundred, K = rows) would occupy a handful of CUs: split K
+        int z = 1;
+        if (tiles < 256 && K >= 512) z = (int)std::min<int64_t>(std::max<int64_t>(512 / tiles, 1), K / 256);
+        if (z > 1) {
+            const int kchunk = ((K + z - 1) / z + GK - 1) / GK * GK;
+            z = (K + kchunk - 1) / kchunk;
+            const int64_t mn = (int64_t)M * N;
+            float *part = workspace(mn * z);
+            if (!part) return hipErrorOutOfMemory;
+            g.z = z;
+            hipLaunchKernelGGL(gemm_kernel, g, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, part, (int64_t)N, 0.f,
+                               (const float *)nullptr, kchunk, mn);
+            hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid_for(mn)), dim3(256), 0, st, M, N, z, (const float *)part, c,
+                               ldc, beta, bias);
+            return hipGetLastError();
+        }
+        hipLaunchKernelGGL(gemm_kernel, g, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, c, ldc, beta, bias, K,
+                           (int64_t)0);
+        return hipGetLastError();
+    }
+    // db[n] += sum_m dy[m*ld + n], rows split over workgroups, slices reduced in order
+    hipError_t colsum(int64_t M, int N, const float *dy, int64_t ld, float *db)
+    {
+        const int64_t rchunk = 256;
+        const int z = (int)std::min<int64_t>((M + rchunk - 1) / rchunk, 65535);
+        const int64_t rc = (M + z - 1) / z;
+        float *part = workspace((int64_t)z * N);
+        if (!part) return hipErrorOutOfMemory;
+        hipLaunchKernelGGL(colsum_part_kernel, dim3((N + 63) / 64, z), dim3(256), 0, st, M, N, dy, ld, rc, part);
+        hipLaunchKernelGGL(colsum_reduce_kernel, dim3((N + 255) / 256), dim3(256), 0, st, N, z, (const float *)part, db);
         return hipGetLastError();
     }
     // Y[B][N] = X[B][K] W[N][K]^T + b   (X rows of stride ldx; W rows of stride ldw, starting at column koff)
@@ -434,8 +523,7 @@ struct Trainer {
     }
     hipError_t bias_bwd(int64_t B, const TrainLin &L, const float *dy)
     {
-        hipLaunchKernelGGL(colsum_kernel, dim3((L.n + 63) / 64), dim3(256), 0, st, B, L.n, dy, (int64_t)L.n, G + L.b);
-        return hipGetLastError();
+        return colsum(B, L.n, dy, (int64_t)L.n, G + L.b);
     }
     void mish(int64_t n, const float *pre, float *out)
     {
@@ -539,8 +627,8 @@ struct Trainer {
             case UOP_CONV: {
                 const int cb = o.in1 >= 0 ? tC(o.in1) : 0, K = (Ci + cb) * o.k;
                 const int64_t R = B * Lo;
-                hipLaunchKernelGGL(colsum_kernel, dim3((Co + 63) / 64), dim3(256), 0, st, R, Co, go, (int64_t)Co, G + o.b);
-                e = gemm(Co, K, (int)R, go, 1, Co, ucol[i], K, 1, G + o.w, K, 1.f, nullptr);
+                e = colsum(R, Co, go, (int64_t)Co, G + o.b);
+                if (e == hipSuccess) e = gemm(Co, K, (int)R, go, 1, Co, ucol[i], K, 1, G + o.w, K, 1.f, nullptr);
                 if (e == hipSuccess && (g0 || g1)) {
                     e = gemm((int)R, K, Co, go, Co, 1, P + o.w, K, 1, ucol[i], K, 0.f, nullptr);
                     hipLaunchKernelGGL(col2im_kernel, dim3(grid_for(B * Li * (Ci + cb))), dim3(256), 0, st, B, Li, Lo, Ci,
@@ -553,18 +641,15 @@ struct Trainer {
                 hipLaunchKernelGGL(convt_scatter_kernel, dim3(grid_for(B * Li * K)), dim3(256), 0, st, B, Li, Lo, Co, o.k,
                                    o.s, o.p, go, ucol[i]);
                 e = gemm(Ci, K, (int)(B * Li), x0, 1, Ci, ucol[i], K, 1, G + o.w, K, 1.f, nullptr);
-                hipLaunchKernelGGL(colsum_kernel, dim3((Co + 63) / 64), dim3(256), 0, st, B * Lo, Co, go, (int64_t)Co,
-                                   G + o.b);
+                if (e == hipSuccess) e = colsum(B * Lo, Co, go, (int64_t)Co, G + o.b);
                 if (e == hipSuccess && g0) e = gemm((int)(B * Li), Ci, K, ucol[i], K, 1, P + o.w, 1, K, g0, Ci, 1.f, nullptr);
                 break;
             }
             case UOP_GN:
                 hipLaunchKernelGGL(gn_bwd_kernel, dim3((unsigned)(B * o.groups)), dim3(256), 0, st, Li, Ci, o.groups, x0, go,
                                    P + o.w, ustat[i], g0, upart[i]);
-                hipLaunchKernelGGL(colsum_kernel, dim3((Ci + 63) / 64), dim3(256), 0, st, B, Ci, upart[i], (int64_t)2 * Ci,
-                                   G + o.w);
-                hipLaunchKernelGGL(colsum_kernel, dim3((Ci + 63) / 64), dim3(256), 0, st, B, Ci, upart[i] + Ci,
-                                   (int64_t)2 * Ci, G + o.b);
+                e = colsum(B, Ci, upart[i], (int64_t)2 * Ci, G + o.w);
+                if (e == hipSuccess) e = colsum(B, Ci, upart[i] + Ci, (int64_t)2 * Ci, G + o.b);
                 break;
             case UOP_MISH: mish_bwd(B * Li * Ci, x0, go, g0, 1); break;
             case UOP_ADDC:
@@ -577,8 +662,8 @@ struct Trainer {
                 break;
             case UOP_LIN: {
                 const int64_t R = B * Li;
-                hipLaunchKernelGGL(colsum_kernel, dim3((Co + 63) / 64), dim3(256), 0, st, R, Co, go, (int64_t)Co, G + o.b);
-                e = gemm(Co, Ci, (int)R, go, 1, Co, x0, Ci, 1, G + o.w, Ci, 1.f, nullptr);
+                e = colsum(R, Co, go, (int64_t)Co, G + o.b);
+                if (e == hipSuccess) e = gemm(Co, Ci, (int)R, go, 1, Co, x0, Ci, 1, G + o.w, Ci, 1.f, nullptr);
                 if (e == hipSuccess && g0) e = gemm((int)R, Ci, Co, go, Co, 1, P + o.w, Ci, 1, g0, Ci, 1.f, nullptr);
                 break;
             }
@@ -732,7 +817,7 @@ struct Trainer {
         mish_bwd(B * W, A.cemb, A.dmc, A.dcemb);
         // time MLP: d t_emb = d c_emb[:, :T] (row stride W)
         if ((e = gemm(sp.t2.n, 128, (int)B, A.dcemb, 1, W, A.q1, 128, 1, G + sp.t2.w, 128, 1.f, nullptr)) != hipSuccess) return e;
-        hipLaunchKernelGGL(colsum_kernel, dim3((T + 63) / 64), dim3(256), 0, st, B, T, A.dcemb, (int64_t)W, G + sp.t2.b);
+        if ((e = colsum(B, T, A.dcemb, (int64_t)W, G + sp.t2.b)) != hipSuccess) return e;
         if ((e = gemm((int)B, 128, T, A.dcemb, W, 1, P + sp.t2.w, 128, 1, A.dq1, 128, 0.f, nullptr)) != hipSuccess) return e;
         mish_bwd(B * 128, A.p1, A.dq1, A.dq1);
         if ((e = bias_bwd(B, sp.t1, A.dq1)) != hipSuccess) return e;
