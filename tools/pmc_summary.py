@@ -10,15 +10,16 @@ import json
 import sys
 
 
-def vals(d, counter):
-    rows = list(csv.DictReader(open(d + "/run_counter_collection.csv")))
+def vals(d, counter, only=None):
+    """per-launch values of one counter; only: substring the kernel name must contain (e.g. "32, 8>")"""
+    rows = [r for r in csv.DictReader(open(d + "/run_counter_collection.csv")) if not only or only in r["Kernel_Name"]]
     v = [float(r["Counter_Value"]) for r in rows if r["Counter_Name"] == counter]
     return v, rows[0]["Kernel_Name"]
 
 
-def main(fetch_dir, write_dir, label, out, algo_bytes=None):
-    f, kname = vals(fetch_dir, "FETCH_SIZE")
-    w, _ = vals(write_dir, "WRITE_SIZE")
+def main(fetch_dir, write_dir, label, out, only=None):
+    f, kname = vals(fetch_dir, "FETCH_SIZE", only)
+    w, _ = vals(write_dir, "WRITE_SIZE", only)
     warm_f = sum(f[1:]) / len(f[1:])
     warm_w = sum(w[1:]) / len(w[1:])
     res = {"kernel": kname, "label": label,
@@ -28,8 +29,8 @@ def main(fetch_dir, write_dir, label, out, algo_bytes=None):
            "hbm_bytes_per_launch": int((2 * warm_f + warm_w) * 1024),
            "hbm_bytes_cold_first_launch": int((2 * f[0] + w[0]) * 1024),
            "hbm_bytes_note": "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 averaged over the warm launches (2..n)"}
-    if algo_bytes:
-        res["algorithmic_bytes_per_launch"] = int(algo_bytes)
+    if only:
+        res["kernel_filter"] = only
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
