@@ -266,6 +266,12 @@ int mpcd_trainer_step(mpcd_trainer *tr, const float *x0, const float *context, c
                       const float *context_mask, int64_t batch, int32_t update, double *loss, void *hip_stream);
 /* which: 0 parameters, 1 EMA parameters, 2 last gradients, 3 Adam exp_avg, 4 Adam exp_avg_sq (host copy) */
 int mpcd_trainer_params(mpcd_trainer *tr, int32_t which, float *host_out, size_t n_floats);
+/* Data-parallel training: each rank steps on its own rows; the flat gradient is sum-all-reduced over the
+ * communicator and divided by nranks before Adam (DistributedDataParallel's averaging), so all ranks keep
+ * identical parameters and EMA. RCCL (one process per GPU; id from mpcd_comm_unique_id) or an in-process
+ * loopback group of nranks trainers on one GPU, each stepped from its own host thread. */
+int mpcd_trainer_comm_init(mpcd_trainer *tr, int32_t nranks, int32_t rank, const void *unique_id);
+int mpcd_trainer_comm_init_loopback(mpcd_trainer *tr, int32_t nranks, int32_t rank, uint64_t group_key);
 void mpcd_trainer_destroy(mpcd_trainer *tr);
 int mpcd_comm_info(mpcd_ctx *ctx, int32_t *nranks, int32_t *rank);  /* 1, 0 without mpcd_comm_init */
 /* recv [nranks * count_per_rank] (rank order); without a communicator: a device copy. */

@@ -123,6 +123,8 @@ EXPORTS = {
                            ctypes.c_void_p], ctypes.c_int),
     "mpcd_trainer_params": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t], ctypes.c_int),
     "mpcd_trainer_destroy": ([ctypes.c_void_p], None),
+    "mpcd_trainer_comm_init": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p], ctypes.c_int),
+    "mpcd_trainer_comm_init_loopback": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64], ctypes.c_int),
     "mpcd_select": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
 }

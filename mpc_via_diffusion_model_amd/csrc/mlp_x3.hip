@@ -48,6 +48,9 @@ constexpr int ROWS_MAX = 32;
 #ifndef MPCD_X3_PAIR_MIN
 #define MPCD_X3_PAIR_MIN 128
 #endif
+#ifndef MPCD_X3_LEAD2
+#define MPCD_X3_LEAD2 0
+#endif
 #ifndef MPCD_X3_XALL
 #define MPCD_X3_XALL 0
 #endif
@@ -647,14 +650,23 @@ struct MlpX3 {
             layer<3>(w3, lds, wave, lane);
             WFrag3<A::K[5], A::N[5], mode_for<A::N[5], R, W>()> w5;
             load_w3(w5, wptr(5), wave, lane16);
+            WFrag3<A::K[6], A::N[6], mode_for<A::N[6], R, W>()> w6;
+#if MPCD_X3_LEAD2  // the 128-wide layers' weights two segments ahead (their L2 latency outlasts one segment)
+            load_w3(w6, wptr(6), wave, lane16);
+#endif
             bar(4);
             layer<4>(w4, lds, wave, lane);
-            WFrag3<A::K[6], A::N[6], mode_for<A::N[6], R, W>()> w6;
+            WFrag3<A::K[7], A::N[7], mode_for<A::N[7], R, W>()> w7;
+#if MPCD_X3_LEAD2
+            load_w3(w7, wptr(7), wave, lane16);
+#else
             load_w3(w6, wptr(6), wave, lane16);
+#endif
             bar(5);
             layer<5>(w5, lds, wave, lane);
-            WFrag3<A::K[7], A::N[7], mode_for<A::N[7], R, W>()> w7;
+#if !MPCD_X3_LEAD2
             load_w3(w7, wptr(7), wave, lane16);
+#endif
             bar(6);
             layer<6>(w6, lds, wave, lane);
             WFrag3<A::K[8], A::N[8], mode_for<A::N[8], R, W>()> w8;

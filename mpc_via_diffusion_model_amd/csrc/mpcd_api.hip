@@ -1274,6 +1274,32 @@ int mpcd_trainer_params(mpcd_trainer *tr, int32_t which, float *host_out, size_t
     return MPCD_OK;
 }
 
+int mpcd_trainer_comm_init(mpcd_trainer *tr, int32_t nranks, int32_t rank, const void *id_in)
+{
+    if (!tr || !id_in || nranks < 1 || rank < 0 || rank >= nranks) return fail(MPCD_EINVAL, "bad comm arguments");
+    std::string e;
+    Comm *c = nullptr;
+    if (int rc = comm_create_rccl(nranks, rank, id_in, &c, e)) return fail(rc, "%s", e.c_str());
+    if (trainer_set_comm(tr->t, c)) {
+        delete c;
+        return fail(MPCD_ESTATE, "trainer communicator already initialised");
+    }
+    return MPCD_OK;
+}
+
+int mpcd_trainer_comm_init_loopback(mpcd_trainer *tr, int32_t nranks, int32_t rank, uint64_t group_key)
+{
+    if (!tr || nranks < 1 || rank < 0 || rank >= nranks) return fail(MPCD_EINVAL, "bad comm arguments");
+    std::string e;
+    Comm *c = nullptr;
+    if (int rc = comm_create_loopback(nranks, rank, group_key, &c, e)) return fail(rc, "%s", e.c_str());
+    if (trainer_set_comm(tr->t, c)) {
+        delete c;
+        return fail(MPCD_ESTATE, "trainer communicator already initialised");
+    }
+    return MPCD_OK;
+}
+
 void mpcd_trainer_destroy(mpcd_trainer *tr)
 {
     if (!tr) return;

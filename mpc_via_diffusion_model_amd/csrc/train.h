@@ -52,3 +52,5 @@ int trainer_step(Trainer *t, const TrainBatch &b, bool update, double *loss, std
 int trainer_read(Trainer *t, int which, float *host, size_t n);
 int64_t trainer_steps(Trainer *t);
 void trainer_free(Trainer *t);
+struct Comm;
+int trainer_set_comm(Trainer *t, Comm *c);  // takes ownership; -1 if one is set already

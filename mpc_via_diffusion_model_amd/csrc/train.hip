@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "comm.h"
 #include "train.h"
 
 namespace {
@@ -421,6 +422,11 @@ __global__ void adam_kernel(int64_t n, float *p, const float *g, float *m, float
     }
 }
 
+__global__ void scale_kernel(int64_t n, float *g, float f)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) g[i] *= f;
+}
+
 // EMA.update_average: old * beta + (1 - beta) * new
 __global__ void ema_kernel(int64_t n, float *ema, const float *p, float beta, int reset)
 {
@@ -442,12 +448,17 @@ struct Trainer {
     std::vector<float *> bufs;
     double *part = nullptr;
     int64_t step = 0;
+    // data parallelism: every rank trains on its own rows; the flat gradient is sum-all-reduced and divided
+    // by the rank count before Adam, so the ranks' parameters stay identical (DistributedDataParallel's rule)
+    Comm *comm = nullptr;
+    std::string comm_err;
 
     ~Trainer()
     {
         for (float *b : bufs) (void)hipFree(b);
         for (float *b : {P, G, Mo, Vo, E, sched, ws}) (void)hipFree(b);
         (void)hipFree(part);
+        delete comm;
     }
     float *alloc(int64_t n)
     {
@@ -822,6 +833,13 @@ struct Trainer {
         mish_bwd(B * 128, A.p1, A.dq1, A.dq1);
         if ((e = bias_bwd(B, sp.t1, A.dq1)) != hipSuccess) return e;
         if ((e = lin_bwd(B, A.e, 32, sp.t1, 0, 32, A.dq1, nullptr, 0.f)) != hipSuccess) return e;
+        // ---- data-parallel gradient average: one all-reduce of the whole flat gradient (a single bucket:
+        // 0.6 MB for the cfg2 MLP, 4 MB for the cart-pole U-Net, tens of microseconds over xGMI)
+        if (comm && comm->nranks > 1) {
+            if (comm->allreduce(G, (size_t)sp.n_params, COMM_SUM_F32, st, comm_err) != 0) return hipErrorUnknown;
+            hipLaunchKernelGGL(scale_kernel, dim3(grid_for(sp.n_params)), dim3(256), 0, st, (int64_t)sp.n_params, G,
+                               1.f / (float)comm->nranks);
+        }
         // ---- Adam, then the EMA model (trainer.py: optimizer step, then every update_ema_every steps)
         ++step;
         const double bc1 = 1.0 - std::pow((double)sp.beta1, (double)step), bc2 = 1.0 - std::pow((double)sp.beta2, (double)step);
@@ -870,9 +888,17 @@ int trainer_step(Trainer *t, const TrainBatch &b, bool update, double *loss, std
     }
     const hipError_t e = t->run(b.batch, b.x0, b.ctx, b.t, b.noise, b.mask, update, loss);
     if (e != hipSuccess) {
-        if (why) *why = std::string("trainer: ") + hipGetErrorString(e);
+        if (why) *why = !t->comm_err.empty() ? "trainer: gradient all-reduce: " + t->comm_err
+                                             : std::string("trainer: ") + hipGetErrorString(e);
         return -2;
     }
+    return 0;
+}
+
+int trainer_set_comm(Trainer *t, Comm *c)
+{
+    if (t->comm) return -1;
+    t->comm = c;
     return 0;
 }
 

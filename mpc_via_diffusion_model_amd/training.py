@@ -43,6 +43,30 @@ class DiffusionTrainer:
                                               ctypes.c_void_p(s1m.data_ptr()), self.n_steps, ctypes.byref(self._tr)),
                 "mpcd_trainer_create")
 
+    def data_parallel(self, group=None, loopback=None):
+        """Average gradients over ranks before each Adam step (DistributedDataParallel's rule) through an RCCL
+        communicator of this trainer: rank 0's unique id is shipped over the torch.distributed group (one
+        process per GPU). loopback=(nranks, rank, key): a virtual rank of an in-process group on one GPU
+        instead (each trainer stepped from its own host thread)."""
+        if loopback is not None:
+            n, r, key = (int(v) for v in loopback)
+            N.check(self._lib.mpcd_trainer_comm_init_loopback(self._tr, n, r, key), "mpcd_trainer_comm_init_loopback")
+            self.world = (r, n)
+            return self
+        import torch.distributed as dist
+        from .distributed import world
+        r, n = world(group)
+        if n > 1:
+            uid = (ctypes.c_uint8 * N.MPCD_COMM_ID_BYTES)()
+            if r == 0:
+                N.check(self._lib.mpcd_comm_unique_id(uid), "mpcd_comm_unique_id")
+            obj = [bytes(uid)]
+            dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+            uid = (ctypes.c_uint8 * N.MPCD_COMM_ID_BYTES).from_buffer_copy(obj[0])
+            N.check(self._lib.mpcd_trainer_comm_init(self._tr, n, r, uid), "mpcd_trainer_comm_init")
+        self.world = (r, n)
+        return self
+
     def close(self):
         if getattr(self, "_tr", None) and self._tr.value:
             self._lib.mpcd_trainer_destroy(self._tr)

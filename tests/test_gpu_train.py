@@ -134,3 +134,56 @@ def test_rejects_bad_inputs():
         tr.loss(x0, ctx[:, :3], t, noise, mask)
     with pytest.raises(ValueError):
         DiffusionTrainer(NetSpec("unet", 1, 32, 2, cfg=False), {}, n_diffusion_steps=10)
+
+
+@pytest.mark.parametrize("kind,shape", [("mlp", (2, 32, 4)), ("unet", (1, 32, 5))])
+def test_data_parallel_loopback_equals_full_batch(kind, shape):
+    """2 virtual ranks (mpcd_trainer_comm_init_loopback, one host thread and stream each) stepping on the two
+    halves of a batch == one trainer on the whole batch: the all-reduced, rank-averaged gradient is the
+    full-batch gradient, and both ranks hold bit-identical parameters afterwards."""
+    import random
+    import threading
+    d, H, C = shape
+    B = 64 if kind == "unet" else 256
+    net = (make_mlp(d, H, C, seed=4) if kind == "mlp" else make_unet(d, C, seed=4)).train()
+    tables = osch.buffers("exponential", 100)
+    spec = NetSpec(kind, d, H, C)
+    full = DiffusionTrainer(spec, net.state_dict(), tables=tables)
+    ranks = [DiffusionTrainer(spec, net.state_dict(), tables=tables) for _ in range(2)]
+    key = random.getrandbits(48)
+    for r, tr in enumerate(ranks):
+        tr.data_parallel(loopback=(2, r, key))
+    g = torch.Generator().manual_seed(9)
+    x0 = torch.rand(B, H, d, generator=g) * 2 - 1
+    ctx = torch.rand(B, C, generator=g) * 2 - 1
+    half = B // 2
+    for step in range(3):
+        t, noise, mask = full.draw(B, (B, H, d), generator=g)
+        full.train_step(x0, ctx, t, noise, mask)
+        errs = []
+
+        def body(r):
+            try:
+                torch.cuda.set_device(0)
+                with torch.cuda.stream(torch.cuda.Stream()):
+                    sl = slice(r * half, (r + 1) * half)
+                    ranks[r].train_step(x0[sl], ctx[sl], t[sl], noise[sl], mask[sl])
+                    torch.cuda.current_stream().synchronize()
+            except BaseException as e:  # noqa: BLE001
+                errs.append(e)
+
+        ts = [threading.Thread(target=body, args=(r,)) for r in range(2)]
+        for th in ts:
+            th.start()
+        for th in ts:
+            th.join(timeout=120)
+        assert not any(th.is_alive() for th in ts), "a virtual rank hung"
+        if errs:
+            raise errs[0]
+        gf, g0, g1 = full.state_dict("grads"), ranks[0].state_dict("grads"), ranks[1].state_dict("grads")
+        for n in gf:
+            assert torch.equal(g0[n], g1[n]), (step, n)
+            if float(gf[n].norm()) > 0:
+                assert _rel(g0[n], gf[n]) <= 1e-5, (step, n, _rel(g0[n], gf[n]))
+        p0, p1 = ranks[0].state_dict("params"), ranks[1].state_dict("params")
+        assert all(torch.equal(p0[n], p1[n]) for n in p0)
