@@ -54,6 +54,13 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 constexpr int MT = 256;  // threads per workgroup
 // weight chunks in flight for the small f16 tiles (NN x NC <= 8): the GEMM phase of a 4-row block
 // streams the whole layer's weights from L2 for 64 columns, so its A loads are latency-bound
+// 16-byte staging loads / epilogue items each thread keeps in flight
+#ifndef MPCD_MX_SU
+#define MPCD_MX_SU 4
+#endif
+#ifndef MPCD_MX_EU
+#define MPCD_MX_EU 4
+#endif
 #ifndef MPCD_MX_DA_SMALL
 #define MPCD_MX_DA_SMALL 4
 #endif
@@ -278,7 +285,7 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
     };
     auto stage_direct = [&](int64_t r0, int nrow) {
         if ((a.ca & 7) == 0 && (a.cb & 7) == 0) {
-            constexpr int SU = 4;  // items per thread in flight before any conversion or LDS store
+            constexpr int SU = MPCD_MX_SU;  // items per thread in flight before any conversion or LDS store
             for (int i0 = tid; i0 < n_items; i0 += SU * MT) {
                 f32x4 lo[SU], hi[SU];
                 int dst[SU];
@@ -531,7 +538,7 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
     };
     auto epilogue = [&](int64_t r0, int nrow) {
         const int n_ro = nrow * a.lout;
-        constexpr int EU = 4;  // items per thread with their residual loads in flight together
+        constexpr int EU = MPCD_MX_EU;  // items per thread with their residual loads in flight together
         for (int i0 = tid < tps * cq ? tid / cq : n_ro; i0 < n_ro; i0 += EU * tps) {
             f32x4 rv[EU];
             int rr[EU], oo_[EU];

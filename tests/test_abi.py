@@ -85,3 +85,28 @@ def test_gemm_numerics_selection_is_validated():
         assert L.mpcd_net_param_count(ctypes.byref(d), ctypes.byref(nt), ctypes.byref(nf)) == want, spec
     with pytest.raises(ValueError):
         NetSpec("mlp", 2, 32, 4, dtype="bf16").desc()
+
+
+def test_trainer_argument_checks():
+    """mpcd_trainer_create rejects bad arguments on the host, before any device work."""
+    L = N.lib()
+    cfg = N.TrainCfg(3e-3, 0.9, 0.999, 1e-8, 0.995, 1000, 10)
+    sched = (ctypes.c_float * 10)(*([0.5] * 10))
+    tr = ctypes.c_void_p()
+    d = NetSpec("mlp", 2, 16, 4).desc()
+    nt, nf = ctypes.c_int32(), ctypes.c_int64()
+    assert L.mpcd_net_param_count(ctypes.byref(d), ctypes.byref(nt), ctypes.byref(nf)) == 0
+    params = (ctypes.c_float * (nf.value + 1))()
+    # wrong parameter count
+    assert L.mpcd_trainer_create(ctypes.byref(d), params, nf.value + 1, ctypes.byref(cfg), sched, sched, 10,
+                                 ctypes.byref(tr)) == -1
+    assert b"floats" in L.mpcd_last_error()
+    # no schedule
+    assert L.mpcd_trainer_create(ctypes.byref(d), params, nf.value, ctypes.byref(cfg), None, sched, 10,
+                                 ctypes.byref(tr)) == -1
+    # the 3-arg TemporalUnet has no CFG mask to train with
+    u = NetSpec("unet", 1, 32, 0, cfg=False).desc()
+    assert L.mpcd_trainer_create(ctypes.byref(u), params, nf.value, ctypes.byref(cfg), sched, sched, 10,
+                                 ctypes.byref(tr)) == -5
+    assert not tr.value
+    assert L.mpcd_trainer_step(None, None, None, None, None, None, 0, 1, None, None) == -1
