@@ -767,7 +767,12 @@ hipError_t launch_one(const ConvMK2 &k2, size_t lds, hipStream_t st)
             return hipGetLastError();
         }
     }
-    hipLaunchKernelGGL((conv_mx_kernel<KIND, P, NN, NC, PERS, NPH>), dim3((unsigned)blocks), dim3(MT), lds, st, k2);
+    static const size_t lds_pad = [] {  // experiment knob: extra LDS per workgroup (fewer co-resident workgroups)
+        const char *e = getenv("MPCD_UNET_LDS_PAD");
+        return e ? (size_t)atol(e) : (size_t)0;
+    }();
+    hipLaunchKernelGGL((conv_mx_kernel<KIND, P, NN, NC, PERS, NPH>), dim3((unsigned)blocks), dim3(MT),
+                       std::min(lds + lds_pad, (size_t)160 * 1024), st, k2);
     return hipGetLastError();
 }
 
