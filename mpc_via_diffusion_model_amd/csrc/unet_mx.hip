@@ -61,6 +61,9 @@ constexpr int MT = 256;  // threads per workgroup
 #ifndef MPCD_MX_EU
 #define MPCD_MX_EU 4
 #endif
+#ifndef MPCD_MX_TILE_H
+#define MPCD_MX_TILE_H 0
+#endif
 #ifndef MPCD_MX_DA_SMALL
 #define MPCD_MX_DA_SMALL 4
 #endif
@@ -189,7 +192,7 @@ struct ConvMK2 {
 };
 
 template <int KIND, int P, int NN, int NC, bool PERS, int NPH>
-__global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
+__device__ __forceinline__ void conv_mx_body(const ConvMK2 &as)
 {
     extern __shared__ __attribute__((aligned(16))) char sm[];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -348,8 +351,16 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
     const int npj = (NT + NN - 1) / NN, ncg = (ctp + NC - 1) / NC;
     const int jobs = npj * ncg * npar;
     const int col = lane & 15, q = lane >> 4;
-    const int sout = a.coutp + 4;
-    float *s_out = reinterpret_cast<float *>(sm + a.out_off);
+    // pre-norm output tile in LDS: fp32, or fp16 for the fp16-operand net when MPCD_MX_TILE_H (half the LDS,
+    // so more workgroups share a CU; the conv's fp32 accumulators are rounded once to fp16 there)
+    using tile_t = typename std::conditional<P == 1 && MPCD_MX_TILE_H, _Float16, float>::type;
+    constexpr int TPAD = sizeof(tile_t) == 2 ? 8 : 4;
+    const int sout = a.coutp + TPAD;
+    tile_t *s_out = reinterpret_cast<tile_t *>(sm + a.out_off);
+    auto tile_ld4 = [&](const tile_t *p) -> f32x4 {
+        if constexpr (sizeof(tile_t) == 2) return __builtin_convertvector(*reinterpret_cast<const f16x4 *>(p), f32x4);
+        else return *reinterpret_cast<const f32x4 *>(p);
+    };
 
     const uint64_t wa = (uint64_t)a.w;
     const uint32_t wlo = __builtin_amdgcn_readfirstlane((uint32_t)wa), whi = __builtin_amdgcn_readfirstlane((uint32_t)(wa >> 32));
@@ -470,8 +481,9 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
             for (int cc = 0; cc < NC; ++cc) {
                 const int ct = cg * NC + cc;
                 if (ct >= ctp) continue;
-                *reinterpret_cast<f32x4 *>(s_out + (size_t)(par * cpar16 + ct * 16 + col) * sout + nt * 16 + 4 * q) =
-                    acc[j][cc];
+                tile_t *dst = s_out + (size_t)(par * cpar16 + ct * 16 + col) * sout + nt * 16 + 4 * q;
+                if constexpr (sizeof(tile_t) == 2) *reinterpret_cast<f16x4 *>(dst) = __builtin_convertvector(acc[j][cc], f16x4);
+                else *reinterpret_cast<f32x4 *>(dst) = acc[j][cc];
             }
         }
     };
@@ -494,12 +506,12 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
         using sum_t = typename std::conditional<P == 1, float, double>::type;
         for (int pi = tid / TPP; pi < pairs; pi += MT / TPP) {
             const int r = pi / a.groups, g = pi - r * a.groups;
-            const float *base = s_out + (g << gsh);
-            const float ref = base[(size_t)colof(r, 0) * sout];
+            const tile_t *base = s_out + (g << gsh);
+            const float ref = (float)base[(size_t)colof(r, 0) * sout];
             sum_t s1 = 0, s2 = 0;
             for (int e = sub; e < nq; e += TPP) {
                 const int oo = e >> (gsh - 2), cc = (e - (oo << (gsh - 2))) * 4;
-                const f32x4 v4 = *reinterpret_cast<const f32x4 *>(base + (size_t)colof(r, oo) * sout + cc);
+                const f32x4 v4 = tile_ld4(base + (size_t)colof(r, oo) * sout + cc);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const sum_t v = (sum_t)v4[k] - (sum_t)ref;
@@ -562,7 +574,7 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
             for (int u = 0; u < EU; ++u) {
                 if (i0 + u * tps >= n_ro) break;
                 const int r = rr[u], oo = oo_[u];
-                const f32x4 raw = *reinterpret_cast<const f32x4 *>(s_out + (size_t)colof(r, oo) * sout + co_t);
+                const f32x4 raw = tile_ld4(s_out + (size_t)colof(r, oo) * sout + co_t);
                 const int64_t grow = r0 + r;
                 f32x4 v = raw;
                 if (epi != UEPI_BIAS) {
@@ -674,6 +686,37 @@ __global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
     }
 }
 
+template <int KIND, int P, int NN, int NC, bool PERS, int NPH>
+__global__ __launch_bounds__(MT) void conv_mx_kernel(const ConvMK2 as)
+{
+    conv_mx_body<KIND, P, NN, NC, PERS, NPH>(as);
+}
+
+// MPCD_MX_WAVES_EU = w > 0: the fp16-operand net's convs are compiled for w waves per SIMD (w workgroups per
+// CU, register budget 512 / w): a workgroup is latency-bound and throughput grows with co-resident ones
+#ifndef MPCD_MX_WAVES_EU
+#define MPCD_MX_WAVES_EU 0
+#endif
+#if MPCD_MX_WAVES_EU > 0
+template <int KIND, int P, int NN, int NC, bool PERS, int NPH>
+__global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(MPCD_MX_WAVES_EU, 8))) void conv_mx_kernel_w(
+    const ConvMK2 as)
+{
+    conv_mx_body<KIND, P, NN, NC, PERS, NPH>(as);
+}
+#endif
+
+template <int KIND, int P, int NN, int NC, bool PERS, int NPH>
+constexpr auto conv_kernel_ptr()
+{
+#if MPCD_MX_WAVES_EU > 0
+    if constexpr (P == 1 && !PERS && NN * NC <= 8) return &conv_mx_kernel_w<KIND, P, NN, NC, PERS, NPH>;
+    else return &conv_mx_kernel<KIND, P, NN, NC, PERS, NPH>;
+#else
+    return &conv_mx_kernel<KIND, P, NN, NC, PERS, NPH>;
+#endif
+}
+
 // ---- host side
 
 uint16_t bf16_rne(float f)
@@ -710,11 +753,17 @@ constexpr Tile kTiles1[] = {{4, 8}, {2, 8}, {2, 4}, {1, 8}, {1, 4}};
 
 int g_n_cu = 0;  // compute units of the device (persistent grids)
 
+// LDS bytes of the pre-norm output tile (rows x (coutp + pad)), as the kernel lays it out
+size_t tile_bytes(int planes, size_t rows, int coutp)
+{
+    return (planes == 1 && MPCD_MX_TILE_H) ? rows * (size_t)(coutp + 8) * 2 : rows * (size_t)(coutp + 4) * 4;
+}
+
 template <int KIND, int P, int NN, int NC, bool PERS, int NPH = 1>
 hipError_t launch_one(const ConvMK2 &k2, size_t lds, hipStream_t st)
 {
     const ConvMK &k = k2.ph[0];
-    auto *fn = reinterpret_cast<const void *>(&conv_mx_kernel<KIND, P, NN, NC, PERS, NPH>);
+    auto *fn = reinterpret_cast<const void *>(conv_kernel_ptr<KIND, P, NN, NC, PERS, NPH>());
     static bool set = false;
     static int resident = 0;  // workgroups per CU at this kernel's registers and the LDS of its first use
     static size_t resident_lds = 0;
@@ -763,7 +812,8 @@ hipError_t launch_one(const ConvMK2 &k2, size_t lds, hipStream_t st)
             k3.ph[0].stag_units = stag;
             k3.ph[0].stag_ncu = g_n_cu;
             k3.ph[0].stag_slots = resident;
-            hipLaunchKernelGGL((conv_mx_kernel<KIND, P, NN, NC, PERS, NPH>), dim3((unsigned)blocks), dim3(MT), lds, st, k3);
+            auto kfn = conv_kernel_ptr<KIND, P, NN, NC, PERS, NPH>();
+            hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(MT), lds, st, k3);
             return hipGetLastError();
         }
     }
@@ -771,7 +821,8 @@ hipError_t launch_one(const ConvMK2 &k2, size_t lds, hipStream_t st)
         const char *e = getenv("MPCD_UNET_LDS_PAD");
         return e ? (size_t)atol(e) : (size_t)0;
     }();
-    hipLaunchKernelGGL((conv_mx_kernel<KIND, P, NN, NC, PERS, NPH>), dim3((unsigned)blocks), dim3(MT),
+    auto kfn = conv_kernel_ptr<KIND, P, NN, NC, PERS, NPH>();
+    hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(MT),
                        std::min(lds + lds_pad, (size_t)160 * 1024), st, k2);
     return hipGetLastError();
 }
@@ -971,7 +1022,7 @@ hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::
         const int nval = kind == UCONV_UP4 ? rb * k.lin : rb * k.lout;
         const int ctp = (nval + 15) / 16;
         const size_t in_b = (size_t)planes * rb * win * cs;
-        const size_t out_b = (size_t)npar * ctp * 16 * (k.coutp + 4) * 4;
+        const size_t out_b = tile_bytes(planes, (size_t)npar * ctp * 16, k.coutp);
         const size_t stat_b = (size_t)(2 * rb * 32 + 4) * 4 + (size_t)4 * k.coutp * 4;
         MxChoice best{};
         for (int ti = 0; ti < ntiles; ++ti) {
@@ -1267,7 +1318,7 @@ hipError_t unet_launch_mx_rtb(int planes, ConvMK &k1, ConvMK &k2, hipStream_t st
         if (rb > 1 && (int64_t)rb > k1.rows) continue;
         const int ctp = (rb * k1.lout + 15) / 16;
         const size_t in1 = (size_t)planes * rb * win1 * k1.cs, in2 = (size_t)planes * rb * win2 * k2.cs;
-        const size_t out_b = (size_t)ctp * 16 * (k1.coutp + 4) * 4;
+        const size_t out_b = tile_bytes(planes, (size_t)ctp * 16, k1.coutp);
         const size_t stat_b = (size_t)(2 * rb * 32 + 4) * 4 + (size_t)4 * k1.coutp * 4;
         const size_t x_off = in1 + out_b;  // >= out_b: the second tile fits in front of x_off
         const size_t lds = x_off + in2 + stat_b;
