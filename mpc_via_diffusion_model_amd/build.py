@@ -48,7 +48,7 @@ def build(force=False, verbose=False, variant=None, defines=()):
     """variant: build an experiment copy (libmpcd_<variant>.so, objects in _build_<variant>/) with
     extra -D defines; load it with MPCD_LIB=<path>. The default build is the product library."""
     cc = hipcc()
-    out, obj, flags = OUT, OBJ, list(FLAGS)
+    out, obj, flags, extra = OUT, OBJ, list(FLAGS), []
     if variant:
         out = os.path.join(PKG, f"libmpcd_{variant}.so")
         obj = OBJ + "_" + variant
@@ -61,7 +61,7 @@ def build(force=False, verbose=False, variant=None, defines=()):
                 del flags[i]
                 if i > 0 and flags[i - 1] == "-mllvm":
                     del flags[i - 1]
-        flags += os.environ.get("MPCD_EXTRA_FLAGS", "").split()
+        extra = os.environ.get("MPCD_EXTRA_FLAGS", "").split()  # appended last (after SOURCE_FLAGS)
     os.makedirs(obj, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     headers.append(os.path.join(os.path.dirname(PKG), "include", "mpcd.h"))
@@ -70,7 +70,7 @@ def build(force=False, verbose=False, variant=None, defines=()):
         s = os.path.join(CSRC, src)
         o = os.path.join(obj, src.replace(".hip", ".o"))
         if force or _stale(o, [s] + headers):
-            jobs.append([cc] + flags + SOURCE_FLAGS.get(src, []) + ["-c", s, "-o", o])
+            jobs.append([cc] + flags + SOURCE_FLAGS.get(src, []) + extra + ["-c", s, "-o", o])
 
     def run(cmd):
         r = subprocess.run(cmd, capture_output=True, text=True)
