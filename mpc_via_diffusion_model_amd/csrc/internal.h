@@ -53,6 +53,7 @@ void mlp_pack_weights(int d0, const float *const *lin_w, const float *const *lin
 hipError_t launch_mlp_sampler(int d0, int nb, const MlpSampleArgs &a, hipStream_t stream);
 // fp32-accurate split-bf16 variant (mlp_x3.hip); shared or no context only
 int mlp_packed_floats_x3(int d0);
+void mlp_x3_force_layout(int layout);  // mpcd_mlp_force_layout
 void mlp_pack_weights_x3(int d0, const float *const *lin_w, const float *const *lin_b, float *out);
 hipError_t launch_mlp_x3(int d0, int nb, const MlpSampleArgs &a, hipStream_t stream);
 

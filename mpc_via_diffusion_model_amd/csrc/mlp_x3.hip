@@ -24,6 +24,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+
 #include "internal.h"
 #include "mlp_common.h"
 
@@ -763,8 +765,10 @@ hipError_t launch_x3_r(const MlpSampleArgs &a, hipStream_t stream)
 // (fewer than one per CU), 16x4 = two independent 4-wave workgroups per CU, whose barriers and
 // latency chains interleave on each SIMD instead of coinciding. MPCD_MLP_LAYOUT=32x8|16x8|16x4 forces.
 enum { LAYOUT_32x8 = 0, LAYOUT_16x8 = 1, LAYOUT_16x4 = 2 };
+std::atomic<int> g_force_layout{-1};  // mpcd_mlp_force_layout (tests: every layout against the oracle)
 int mlp_x3_layout(int64_t batch, int nb)
 {
+    if (const int f = g_force_layout.load(); f >= 0) return f;
     static const int forced = [] {
         const char *e = getenv("MPCD_MLP_LAYOUT");
         if (!e || !e[0]) return -1;
@@ -811,6 +815,8 @@ hipError_t launch_x3_d0(const MlpSampleArgs &a, hipStream_t stream)
 }
 
 }  // namespace
+
+void mlp_x3_force_layout(int layout) { g_force_layout.store(layout); }
 
 int mlp_packed_floats_x3(int d0)
 {

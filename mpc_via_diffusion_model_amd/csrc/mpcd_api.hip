@@ -745,6 +745,13 @@ int mpcd_unet_force_tiling(int32_t conv_pick, int32_t block_pick)
     return MPCD_OK;
 }
 
+int mpcd_mlp_force_layout(int32_t layout)
+{
+    if (layout < -1 || layout > 2) return fail(MPCD_EINVAL, "layout -1 (auto), 0 (32x8), 1 (16x8) or 2 (16x4)");
+    mlp_x3_force_layout(layout);
+    return MPCD_OK;
+}
+
 int mpcd_last_sample_ms(mpcd_ctx *c, float *ms)
 {
     if (!c || !ms) return fail(MPCD_EINVAL, "null argument");

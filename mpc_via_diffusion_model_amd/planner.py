@@ -50,6 +50,15 @@ def force_unet_tiling(conv=-1, block=-1):
     N.check(N.lib().mpcd_unet_force_tiling(int(conv), int(block)), "mpcd_unet_force_tiling")
 
 
+MLP_LAYOUTS = {"auto": -1, "32x8": 0, "16x8": 1, "16x4": 2}
+
+
+def force_mlp_layout(layout="auto"):
+    """Process-wide MLP sampler workgroup layout (mpcd_mlp_force_layout): "auto" (by batch size), "32x8",
+    "16x8" or "16x4" (rows x waves per workgroup)."""
+    N.check(N.lib().mpcd_mlp_force_layout(MLP_LAYOUTS[layout]), "mpcd_mlp_force_layout")
+
+
 @dataclass
 class NetSpec:
     """Architecture of the noise-net (temporal_unet.py constructor arguments)."""

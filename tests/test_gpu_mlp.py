@@ -162,3 +162,38 @@ def test_f32x3_matches_exact_f32_at_full_size():
     assert torch.isfinite(b).all()
     rel = (a - b).flatten(1).norm(dim=1) / a.flatten(1).norm(dim=1).clamp_min(1e-12)
     assert float(rel.max()) < 1e-4, float(rel.max())
+
+
+@pytest.mark.parametrize("layout", ["32x8", "16x8", "16x4"])
+def test_every_workgroup_layout_matches_oracle(layout):
+    """Each split-bf16 sampler layout (mpcd_mlp_force_layout) against the oracle at the cfg1 shape and a ragged
+    per-candidate-context batch, plus both CFG branches of one eps evaluation; the default picks 16x8 below one
+    32-row workgroup per CU, so without the override the 32x8 headline layout would only meet the oracle at
+    full size through the exact-fp32 kernel."""
+    from mpc_via_diffusion_model_amd.planner import force_mlp_layout
+    force_mlp_layout(layout)
+    try:
+        for B, H, d, C, N, nwo, shared in ((64, 16, 2, 4, 50, 0, True), (100, 32, 2, 4, 100, 5, False)):
+            net = make_mlp(d, H, C)
+            plan = _planner(net, d, H, C, N, dtype="f32x3")
+            ctx = _ctx(B, C, shared)
+            S = N + nwo
+            noise = torch.randn(S + 1, B, H, d, generator=torch.Generator().manual_seed(11))
+            ref = osam.ddpm_cfg(net, osch.buffers("exponential", N), ctx.expand(B, C), 0.01, B, H, nwo, noise=noise,
+                                return_chain=True)
+            got = plan.run_CFG(ctx, None, 0.01, n_samples=B, horizon=H, return_chain=True,
+                               n_diffusion_steps_without_noise=nwo, noise=noise)
+            assert_traj_close(got, ref, what=f"ddpm chain, layout {layout}, B={B}")
+        B, H, d, C = 40, 32, 2, 4
+        net = make_mlp(d, H, C, seed=12)
+        plan = _planner(net, d, H, C, 100, dtype="f32x3")
+        x = torch.randn(B, H, d, generator=torch.Generator().manual_seed(1))
+        ctx = torch.rand(1, C, generator=torch.Generator().manual_seed(2)) * 2 - 1
+        ec, eu = plan.eps(x, 37, ctx)
+        tt = torch.full((B,), 37, dtype=torch.long)
+        with torch.no_grad():
+            rc = net(x, tt, ctx.expand(B, C), torch.zeros(B, 1))
+            ru = net(x, tt, ctx.expand(B, C), torch.ones(B, 1))
+        assert float((ec.cpu() - rc).abs().max()) <= 1e-5 and float((eu.cpu() - ru).abs().max()) <= 1e-5
+    finally:
+        force_mlp_layout("auto")
