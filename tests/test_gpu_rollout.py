@@ -258,3 +258,21 @@ def test_nonfinite_weights_fail_loudly(kind):
     fl = ctypes.c_int32()
     N.check(bad._lib.mpcd_last_step_flags(bad._ctx, ctypes.byref(fl)), "flags")
     assert fl.value & N.MPCD_STEP_NONFINITE_WINNER and fl.value & N.MPCD_STEP_NAN_SAMPLES
+
+
+@pytest.mark.parametrize("layout", ["32x8", "16x8", "16x4"])
+def test_chain_absmax_every_mlp_layout(layout):
+    """The per-candidate chain |x| maxima (the clip rule's input) from every MLP sampler layout, shared context
+    (the split-bf16 sampler's case), ragged batch: equal to the maxima of the chain itself."""
+    from mpc_via_diffusion_model_amd.planner import force_mlp_layout
+    d, H, C, N, B = 2, 16, 4, 25, 45
+    net = make_mlp(d, H, C, seed=7)
+    plan = DiffusionMPC(NetSpec("mlp", d, H, C, dtype="f32x3"), net.state_dict(), n_diffusion_steps=N)
+    ctx = torch.rand(1, C) * 2 - 1
+    am = torch.empty(B, dtype=torch.float32, device="cuda")
+    force_mlp_layout(layout)
+    try:
+        chain = plan.sample_trajectories(ctx, B, H, seed=4, return_chain=True, absmax_out=am)
+    finally:
+        force_mlp_layout("auto")
+    assert torch.equal(am, chain.abs().amax(dim=(0, 2, 3)))
