@@ -94,7 +94,7 @@ __device__ __forceinline__ int n_cols(const ConvK &a)
 }
 
 template <int KIND, int EPI>
-__global__ __launch_bounds__(CT) void conv_kernel(const ConvK a)
+__device__ __forceinline__ void conv_body(const ConvK &a)
 {
     extern __shared__ float sm[];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -258,6 +258,13 @@ __global__ __launch_bounds__(CT) void conv_kernel(const ConvK a)
             for (int e = 0; e < 4 && co + e < a.cout; ++e) dst[e] = v[e];
         }
     }
+}
+
+// the kernel argument reaches the body by reference: it stays in SGPRs, loaded on demand (see unet_mx.hip)
+template <int KIND, int EPI>
+__global__ __launch_bounds__(CT) void conv_kernel(const ConvK a)
+{
+    conv_body<KIND, EPI>(a);
 }
 
 // x_T into the state (and chain[0])
