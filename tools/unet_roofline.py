@@ -74,7 +74,11 @@ def main(cfg, B, H, d, C, dtype, out=None):
             for j in range(p)]
     table = []
     for j in range(p):
-        table.append({"i": j, "kernel": names[-p + j], "us": round(dur[j] * 1e6, 1), "hbm_MB": round(hbm[j] / 1e6, 1),
+        # executed matrix-core FLOPs of the launch: SQ_INSTS_MFMA (per wave) x 16x16x32 x 2
+        fl = ctr[j].get("SQ_INSTS_MFMA", 0) * 16 * 16 * 32 * 2
+        table.append({"i": j, "kernel": names[-p + j], "us": round(dur[j] * 1e6, 1),
+                      "mfma_gflop": round(fl / 1e9, 1), "mfma_frac": round(fl / dur[j] / PEAK_BF16, 3),
+                      "hbm_MB": round(hbm[j] / 1e6, 1),
                       "GB_s": round(hbm[j] / dur[j] / 1e9, 1), "hbm_frac": round(hbm[j] / dur[j] / PEAK_HBM, 3),
                       "mfma_busy": round(busy[j], 3), "mfma_insts": ctr[j].get("SQ_INSTS_MFMA", 0)})
     res = {
@@ -99,10 +103,10 @@ def main(cfg, B, H, d, C, dtype, out=None):
     if out:
         open(out, "w").write(s)
     print(json.dumps({k: v for k, v in res.items() if k != "per_launch"}, indent=1))
-    print(f"{'i':>3} {'kernel':22s} {'us':>8} {'MB':>8} {'GB/s':>8} {'hbm':>6} {'mfma':>6}")
+    print(f"{'i':>3} {'kernel':22s} {'us':>8} {'GFLOP':>8} {'mfma':>6} {'MB':>8} {'GB/s':>8} {'hbm':>6} {'busy':>6}")
     for r in table:
-        print(f"{r['i']:3d} {r['kernel']:22s} {r['us']:8.1f} {r['hbm_MB']:8.1f} {r['GB_s']:8.1f} {r['hbm_frac']:6.3f} "
-              f"{r['mfma_busy']:6.3f}")
+        print(f"{r['i']:3d} {r['kernel']:22s} {r['us']:8.1f} {r['mfma_gflop']:8.1f} {r['mfma_frac']:6.3f} {r['hbm_MB']:8.1f} "
+              f"{r['GB_s']:8.1f} {r['hbm_frac']:6.3f} {r['mfma_busy']:6.3f}")
 
 
 if __name__ == "__main__":
