@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -78,6 +80,64 @@ __global__ __launch_bounds__(256) void gemm_kernel(int M, int N, int K, const fl
             *p = beta != 0.f ? *p + v : v;
         }
     }
+}
+
+// The same contract on the fp32 matrix cores: v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulate).
+// 4 waves, each a 32x32 quarter of the 64x64 tile as 2x2 MFMA tiles; the LDS staging is gemm_kernel's.
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void gemm_mfma_kernel(int M, int N, int K, const float *__restrict__ a, int64_t sam,
+                                                        int64_t sak, const float *__restrict__ b, int64_t sbk,
+                                                        int64_t sbn, float *__restrict__ c, int64_t ldc, float beta,
+                                                        const float *__restrict__ bias, int kchunk, int64_t zstride)
+{
+    __shared__ float As[GK][GT + 1], Bs[GK][GT + 1];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+    const int r16 = lane & 15, kq = lane >> 4;
+    const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
+    const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
+    c += blockIdx.z * zstride;
+    f32x4_t acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = kb; k0 < ke; k0 += GK) {
+        for (int i = threadIdx.x; i < GK * GT; i += 256) {
+            const int kk = i / GT, r = i % GT;
+            const int m = m0 + r, n = n0 + r, k = k0 + kk;
+            As[kk][r] = (m < M && k < ke) ? a[m * sam + k * sak] : 0.f;
+            Bs[kk][r] = (n < N && k < ke) ? b[k * sbk + n * sbn] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < GK; kk += 4) {
+            float af[2], bf[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                af[t] = As[kk + kq][wm + t * 16 + r16];
+                bf[t] = Bs[kk + kq][wn + t * 16 + r16];
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int m = m0 + wm + i * 16 + 4 * kq + e, n = n0 + wn + j * 16 + r16;
+                if (m >= M || n >= N) continue;
+                float v = acc[i][j][e];
+                if (bias) v += bias[n];
+                float *p = c + m * ldc + n;
+                *p = beta != 0.f ? *p + v : v;
+            }
 }
 
 // C[m][n] = beta * C + sum_z part[z][m][n] (+ bias[n])
@@ -482,6 +542,15 @@ struct Trainer {
         }
         return ws;
     }
+    // the fp32 MFMA GEMM (default) or the VALU one (MPCD_TRAIN_GEMM=valu)
+    static decltype(&gemm_kernel) gemm_fn()
+    {
+        static const bool valu = [] {
+            const char *e = getenv("MPCD_TRAIN_GEMM");
+            return e && !strcmp(e, "valu");
+        }();
+        return valu ? &gemm_kernel : &gemm_mfma_kernel;
+    }
     hipError_t gemm(int M, int N, int K, const float *a, int64_t sam, int64_t sak, const float *b, int64_t sbk,
                     int64_t sbn, float *c, int64_t ldc, float beta, const float *bias)
     {
@@ -497,13 +566,13 @@ struct Trainer {
             float *part = workspace(mn * z);
             if (!part) return hipErrorOutOfMemory;
             g.z = z;
-            hipLaunchKernelGGL(gemm_kernel, g, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, part, (int64_t)N, 0.f,
+            hipLaunchKernelGGL(gemm_fn(), g, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, part, (int64_t)N, 0.f,
                                (const float *)nullptr, kchunk, mn);
             hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid_for(mn)), dim3(256), 0, st, M, N, z, (const float *)part, c,
                                ldc, beta, bias);
             return hipGetLastError();
         }
-        hipLaunchKernelGGL(gemm_kernel, g, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, c, ldc, beta, bias, K,
+        hipLaunchKernelGGL(gemm_fn(), g, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, c, ldc, beta, bias, K,
                            (int64_t)0);
         return hipGetLastError();
     }
