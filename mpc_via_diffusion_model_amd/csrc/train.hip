@@ -164,7 +164,16 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(int64_t M, int N, cons
     const int64_t mb = blockIdx.y * rchunk, me = min(M, mb + rchunk);
     float acc = 0.f;
     if (n < N)
-        for (int64_t m = mb + r; m < me; m += 4) acc += dy[m * ld + n];
+        for (int64_t m0 = mb + r; m0 < me; m0 += 4 * 8) {  // 8 independent loads in flight, summed in order
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t m = m0 + 4 * u;
+                v[u] = m < me ? dy[m * ld + n] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += v[u];
+        }
     s[r][c] = acc;
     __syncthreads();
     if (r == 0 && n < N) part[blockIdx.y * (int64_t)N + n] = (s[0][c] + s[1][c]) + (s[2][c] + s[3][c]);
