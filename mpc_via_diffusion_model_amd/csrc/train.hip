@@ -28,6 +28,15 @@ namespace {
 constexpr int GT = 64;   // GEMM tile (rows and columns of C per workgroup)
 constexpr int GK = 16;   // k-step staged in LDS
 
+// rs (optional, the column-0 workgroups): rs[z*M + m] = sum_k A(m,k) over the slice, in k order, from the staged A
+// tile — for dW = dY^T X that is the bias gradient's slice of dY's column sums, without a second pass over dY.
+MPCD_DEV float rowsum_step(const float (&As)[GK][GT + 1], float acc)
+{
+#pragma unroll
+    for (int kk = 0; kk < GK; ++kk) acc += As[kk][threadIdx.x];
+    return acc;
+}
+
 // C[m][n] (ldc) = beta * C + sum_k A(m,k) B(k,n) (+ bias[n]); A(m,k) = a[m*sam + k*sak], B(k,n) = b[k*sbk + n*sbn].
 // 256 threads, each a 4x4 block of C; the k-sum runs in k order per output (fp32 FMA off: -ffp-contract=off).
 // Split K (gridDim.z > 1): slice z sums k in [z*kchunk, (z+1)*kchunk) into c + z*zstride (beta 0, no bias);
@@ -35,7 +44,8 @@ constexpr int GK = 16;   // k-step staged in LDS
 __global__ __launch_bounds__(256) void gemm_kernel(int M, int N, int K, const float *__restrict__ a, int64_t sam,
                                                    int64_t sak, const float *__restrict__ b, int64_t sbk, int64_t sbn,
                                                    float *__restrict__ c, int64_t ldc, float beta,
-                                                   const float *__restrict__ bias, int kchunk, int64_t zstride)
+                                                   const float *__restrict__ bias, int kchunk, int64_t zstride,
+                                                   float *__restrict__ rs)
 {
     __shared__ float As[GK][GT + 1], Bs[GK][GT + 1];
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
@@ -43,6 +53,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(int M, int N, int K, const fl
     const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
     c += blockIdx.z * zstride;
     float acc[4][4] = {};
+    const bool rsum = rs && blockIdx.x == 0 && threadIdx.x < GT;
+    float rsacc = 0.f;
     for (int k0 = kb; k0 < ke; k0 += GK) {
         for (int i = threadIdx.x; i < GK * GT; i += 256) {
             const int kk = i / GT, r = i % GT;
@@ -51,6 +63,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(int M, int N, int K, const fl
             Bs[kk][r] = (n < N && k < ke) ? b[k * sbk + n * sbn] : 0.f;
         }
         __syncthreads();
+        if (rsum) rsacc = rowsum_step(As, rsacc);
 #pragma unroll
         for (int kk = 0; kk < GK; ++kk) {
             float av[4], bv[4];
@@ -66,6 +79,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(int M, int N, int K, const fl
         }
         __syncthreads();
     }
+    if (rsum && m0 + (int)threadIdx.x < M) rs[blockIdx.z * (int64_t)M + m0 + threadIdx.x] = rsacc;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int m = m0 + ty + 16 * i;
@@ -88,7 +102,8 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void gemm_mfma_kernel(int M, int N, int K, const float *__restrict__ a, int64_t sam,
                                                         int64_t sak, const float *__restrict__ b, int64_t sbk,
                                                         int64_t sbn, float *__restrict__ c, int64_t ldc, float beta,
-                                                        const float *__restrict__ bias, int kchunk, int64_t zstride)
+                                                        const float *__restrict__ bias, int kchunk, int64_t zstride,
+                                                        float *__restrict__ rs)
 {
     __shared__ float As[GK][GT + 1], Bs[GK][GT + 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -102,6 +117,8 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(int M, int N, int K, con
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const bool rsum = rs && blockIdx.x == 0 && threadIdx.x < GT;
+    float rsacc = 0.f;
     for (int k0 = kb; k0 < ke; k0 += GK) {
         for (int i = threadIdx.x; i < GK * GT; i += 256) {
             const int kk = i / GT, r = i % GT;
@@ -110,6 +127,7 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(int M, int N, int K, con
             Bs[kk][r] = (n < N && k < ke) ? b[k * sbk + n * sbn] : 0.f;
         }
         __syncthreads();
+        if (rsum) rsacc = rowsum_step(As, rsacc);
 #pragma unroll
         for (int kk = 0; kk < GK; kk += 4) {
             float af[2], bf[2];
@@ -125,6 +143,7 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(int M, int N, int K, con
         }
         __syncthreads();
     }
+    if (rsum && m0 + (int)threadIdx.x < M) rs[blockIdx.z * (int64_t)M + m0 + threadIdx.x] = rsacc;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -561,28 +580,36 @@ struct Trainer {
         return valu ? &gemm_kernel : &gemm_mfma_kernel;
     }
     hipError_t gemm(int M, int N, int K, const float *a, int64_t sam, int64_t sak, const float *b, int64_t sbk,
-                    int64_t sbn, float *c, int64_t ldc, float beta, const float *bias)
+                    int64_t sbn, float *c, int64_t ldc, float beta, const float *bias, float *db = nullptr)
     {
         dim3 g((N + GT - 1) / GT, (M + GT - 1) / GT);
         const int64_t tiles = (int64_t)g.x * g.y;
         // the weight-gradient GEMMs (M, N <= a few hundred, K = rows) would occupy a handful of CUs: split K
         int z = 1;
         if (tiles < 256 && K >= 512) z = (int)std::min<int64_t>(std::max<int64_t>(512 / tiles, 1), K / 256);
+        // db (optional): db[m] += sum_k A(m,k), taken from the staged A tiles (slices reduced in z order)
         if (z > 1) {
             const int kchunk = ((K + z - 1) / z + GK - 1) / GK * GK;
             z = (K + kchunk - 1) / kchunk;
             const int64_t mn = (int64_t)M * N;
-            float *part = workspace(mn * z);
+            float *part = workspace(mn * z + (db ? (int64_t)M * z : 0));
             if (!part) return hipErrorOutOfMemory;
+            float *rs = db ? part + mn * z : nullptr;
             g.z = z;
             hipLaunchKernelGGL(gemm_fn(), g, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, part, (int64_t)N, 0.f,
-                               (const float *)nullptr, kchunk, mn);
+                               (const float *)nullptr, kchunk, mn, rs);
             hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid_for(mn)), dim3(256), 0, st, M, N, z, (const float *)part, c,
                                ldc, beta, bias);
+            if (db)
+                hipLaunchKernelGGL(colsum_reduce_kernel, dim3((M + 255) / 256), dim3(256), 0, st, M, z, (const float *)rs,
+                                   db);
             return hipGetLastError();
         }
+        float *rs = nullptr;
+        if (db && !(rs = workspace(M))) return hipErrorOutOfMemory;
         hipLaunchKernelGGL(gemm_fn(), g, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, c, ldc, beta, bias, K,
-                           (int64_t)0);
+                           (int64_t)0, rs);
+        if (db) hipLaunchKernelGGL(colsum_reduce_kernel, dim3((M + 255) / 256), dim3(256), 0, st, M, 1, (const float *)rs, db);
         return hipGetLastError();
     }
     // db[n] += sum_m dy[m*ld + n], rows split over workgroups, slices reduced in order
@@ -602,17 +629,15 @@ struct Trainer {
     {
         return gemm((int)B, L.n, K, x, ldx, 1, P + L.w + koff, 1, L.k, y, L.n, beta, bias ? P + L.b : nullptr);
     }
-    // backward of Y = X W[:, koff:koff+K]^T: dW[:, koff..] += dY^T X; dX (+)= dY W[:, koff..]
+    // backward of Y = X W[:, koff:koff+K]^T: dW[:, koff..] += dY^T X; dX (+)= dY W[:, koff..];
+    // with_bias: db += column sums of dY, folded into the dW GEMM's staged dY tiles
     hipError_t lin_bwd(int64_t B, const float *x, int ldx, const TrainLin &L, int koff, int K, const float *dy, float *dx,
-                       float dx_beta)
+                       float dx_beta, bool with_bias = false)
     {
-        hipError_t e = gemm(L.n, K, (int)B, dy, 1, L.n, x, ldx, 1, G + L.w + koff, L.k, 1.f, nullptr);
+        hipError_t e = gemm(L.n, K, (int)B, dy, 1, L.n, x, ldx, 1, G + L.w + koff, L.k, 1.f, nullptr,
+                            with_bias ? G + L.b : nullptr);
         if (e == hipSuccess && dx) e = gemm((int)B, K, L.n, dy, L.n, 1, P + L.w + koff, L.k, 1, dx, K, dx_beta, nullptr);
         return e;
-    }
-    hipError_t bias_bwd(int64_t B, const TrainLin &L, const float *dy)
-    {
-        return colsum(B, L.n, dy, (int64_t)L.n, G + L.b);
     }
     void mish(int64_t n, const float *pre, float *out)
     {
@@ -716,8 +741,7 @@ struct Trainer {
             case UOP_CONV: {
                 const int cb = o.in1 >= 0 ? tC(o.in1) : 0, K = (Ci + cb) * o.k;
                 const int64_t R = B * Lo;
-                e = colsum(R, Co, go, (int64_t)Co, G + o.b);
-                if (e == hipSuccess) e = gemm(Co, K, (int)R, go, 1, Co, ucol[i], K, 1, G + o.w, K, 1.f, nullptr);
+                e = gemm(Co, K, (int)R, go, 1, Co, ucol[i], K, 1, G + o.w, K, 1.f, nullptr, G + o.b);
                 if (e == hipSuccess && (g0 || g1)) {
                     e = gemm((int)R, K, Co, go, Co, 1, P + o.w, K, 1, ucol[i], K, 0.f, nullptr);
                     hipLaunchKernelGGL(col2im_kernel, dim3(grid_for(B * Li * (Ci + cb))), dim3(256), 0, st, B, Li, Lo, Ci,
@@ -737,8 +761,12 @@ struct Trainer {
             case UOP_GN:
                 hipLaunchKernelGGL(gn_bwd_kernel, dim3((unsigned)(B * o.groups)), dim3(256), 0, st, Li, Ci, o.groups, x0, go,
                                    P + o.w, ustat[i], g0, upart[i]);
-                e = colsum(B, Ci, upart[i], (int64_t)2 * Ci, G + o.w);
-                if (e == hipSuccess) e = colsum(B, Ci, upart[i] + Ci, (int64_t)2 * Ci, G + o.b);
+                if (o.b == o.w + Ci) {  // weight and bias adjacent in the flat buffer: one pass over [B][2C]
+                    e = colsum(B, 2 * Ci, upart[i], (int64_t)2 * Ci, G + o.w);
+                } else {
+                    e = colsum(B, Ci, upart[i], (int64_t)2 * Ci, G + o.w);
+                    if (e == hipSuccess) e = colsum(B, Ci, upart[i] + Ci, (int64_t)2 * Ci, G + o.b);
+                }
                 break;
             case UOP_MISH: mish_bwd(B * Li * Ci, x0, go, g0, 1); break;
             case UOP_ADDC:
@@ -751,8 +779,7 @@ struct Trainer {
                 break;
             case UOP_LIN: {
                 const int64_t R = B * Li;
-                e = colsum(R, Co, go, (int64_t)Co, G + o.b);
-                if (e == hipSuccess) e = gemm(Co, Ci, (int)R, go, 1, Co, x0, Ci, 1, G + o.w, Ci, 1.f, nullptr);
+                e = gemm(Co, Ci, (int)R, go, 1, Co, x0, Ci, 1, G + o.w, Ci, 1.f, nullptr, G + o.b);
                 if (e == hipSuccess && g0) e = gemm((int)R, Ci, Co, go, Co, 1, P + o.w, Ci, 1, g0, Ci, 1.f, nullptr);
                 break;
             }
@@ -830,17 +857,13 @@ struct Trainer {
         const int W = sp.temb + sp.ctx_dim;
         hipError_t e;
         mish_bwd(B * k.co, A.s[j], A.dy[j], A.dh[j]);  // d s
-        e = bias_bwd(B, k.lb, A.dh[j]);
-        if (e == hipSuccess) e = bias_bwd(B, k.lc, A.dh[j]);
-        if (e == hipSuccess) e = lin_bwd(B, A.mc, W, k.lc, 0, W, A.dh[j], A.dmc, 1.f);
-        if (e == hipSuccess) e = lin_bwd(B, A.h1[j], k.co, k.lb, 0, k.co, A.dh[j], A.tmp, 0.f);  // d h1 -> tmp
+        e = lin_bwd(B, A.mc, W, k.lc, 0, W, A.dh[j], A.dmc, 1.f, true);
+        if (e == hipSuccess) e = lin_bwd(B, A.h1[j], k.co, k.lb, 0, k.co, A.dh[j], A.tmp, 0.f, true);  // d h1 -> tmp
         if (e != hipSuccess) return e;
         mish_bwd(B * k.co, A.a1[j], A.tmp, A.tmp);  // d a1
-        e = bias_bwd(B, k.la, A.tmp);
-        if (e != hipSuccess) return e;
         const float *x0 = k.in0 < 0 ? A.xn : A.y[k.in0];
         const int c0 = k.in0 < 0 ? sp.flat : sp.blocks[k.in0].co;
-        e = lin_bwd(B, x0, c0, k.la, 0, c0, A.tmp, k.in0 < 0 ? nullptr : A.dy[k.in0], 1.f);
+        e = lin_bwd(B, x0, c0, k.la, 0, c0, A.tmp, k.in0 < 0 ? nullptr : A.dy[k.in0], 1.f, true);
         if (e == hipSuccess && k.in1 >= 0)
             e = lin_bwd(B, A.y[k.in1], sp.blocks[k.in1].co, k.la, c0, sp.blocks[k.in1].co, A.tmp, A.dy[k.in1], 1.f);
         return e;
@@ -896,21 +919,20 @@ struct Trainer {
                     return e;
             if ((e = unet_bwd(B)) != hipSuccess) return e;
         } else {
-            if ((e = bias_bwd(B, sp.f2, A.dout)) != hipSuccess) return e;
-            if ((e = lin_bwd(B, A.f1, sp.base, sp.f2, 0, sp.base, A.dout, A.tmp, 0.f)) != hipSuccess) return e;  // d f1
-            if ((e = bias_bwd(B, sp.f1, A.tmp)) != hipSuccess) return e;
-            if ((e = lin_bwd(B, A.y[last], sp.base, sp.f1, 0, sp.base, A.tmp, A.dy[last], 1.f)) != hipSuccess) return e;
+            if ((e = lin_bwd(B, A.f1, sp.base, sp.f2, 0, sp.base, A.dout, A.tmp, 0.f, true)) != hipSuccess) return e;  // d f1
+            if ((e = lin_bwd(B, A.y[last], sp.base, sp.f1, 0, sp.base, A.tmp, A.dy[last], 1.f, true)) != hipSuccess)
+                return e;
             for (int j = nb - 1; j >= 0; --j)
                 if ((e = block_bwd(B, j)) != hipSuccess) return e;
         }
         mish_bwd(B * W, A.cemb, A.dmc, A.dcemb);
         // time MLP: d t_emb = d c_emb[:, :T] (row stride W)
-        if ((e = gemm(sp.t2.n, 128, (int)B, A.dcemb, 1, W, A.q1, 128, 1, G + sp.t2.w, 128, 1.f, nullptr)) != hipSuccess) return e;
-        if ((e = colsum(B, T, A.dcemb, (int64_t)W, G + sp.t2.b)) != hipSuccess) return e;
+        if ((e = gemm(sp.t2.n, 128, (int)B, A.dcemb, 1, W, A.q1, 128, 1, G + sp.t2.w, 128, 1.f, nullptr, G + sp.t2.b)) !=
+            hipSuccess)
+            return e;
         if ((e = gemm((int)B, 128, T, A.dcemb, W, 1, P + sp.t2.w, 128, 1, A.dq1, 128, 0.f, nullptr)) != hipSuccess) return e;
         mish_bwd(B * 128, A.p1, A.dq1, A.dq1);
-        if ((e = bias_bwd(B, sp.t1, A.dq1)) != hipSuccess) return e;
-        if ((e = lin_bwd(B, A.e, 32, sp.t1, 0, 32, A.dq1, nullptr, 0.f)) != hipSuccess) return e;
+        if ((e = lin_bwd(B, A.e, 32, sp.t1, 0, 32, A.dq1, nullptr, 0.f, true)) != hipSuccess) return e;
         // ---- data-parallel gradient average: one all-reduce of the whole flat gradient (a single bucket:
         // 0.6 MB for the cfg2 MLP, 4 MB for the cart-pole U-Net, tens of microseconds over xGMI)
         if (comm && comm->nranks > 1) {

@@ -126,6 +126,24 @@ def test_unet_loss_grads_step(shape):
         assert torch.allclose((params[n] - p0[n])[sure], (p - p0[n])[sure], rtol=1e-3, atol=1e-6 * lr), n
 
 
+@pytest.mark.parametrize("kind,shape", [("mlp", (2, 32, 4, 1024)), ("unet", (1, 32, 5, 640))])
+def test_grads_at_split_k_batches(kind, shape):
+    """Batches large enough that the weight-gradient GEMMs over the batch rows split K (K >= 512): the bias
+    gradients folded into those GEMMs' staged dY tiles are reduced over the K slices, checked with every other
+    gradient against the oracle."""
+    d, H, C, B = shape
+    tr, orc, batch = _setup(d, H, C, B, kind=kind)
+    ref_loss = orc.train_step(*batch)
+    got_loss = tr.train_step(*batch)
+    assert abs(got_loss - ref_loss) <= 1e-5 * abs(ref_loss)
+    grads = tr.state_dict("grads")
+    for n, p in orc.net.named_parameters():
+        if float(p.grad.norm()) == 0.0:
+            assert float(grads[n].norm()) == 0.0, n
+            continue
+        assert _rel(grads[n], p.grad) <= 1e-4, (n, _rel(grads[n], p.grad))
+
+
 def test_rejects_bad_inputs():
     tr, _, (x0, ctx, t, noise, mask) = _setup(2, 16, 4, 8)
     with pytest.raises(ValueError):
