@@ -119,14 +119,29 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(int M, int N, int K, con
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     const bool rsum = rs && blockIdx.x == 0 && threadIdx.x < GT;
     float rsacc = 0.f;
+    // register double buffer: the next k-step's operands are loaded while this one's MFMAs run
+    constexpr int PT = GK * GT / 256;
+    const int sr = threadIdx.x % GT, sk = threadIdx.x / GT;
+    const bool mok = m0 + sr < M, nok = n0 + sr < N;
+    const float *ap = a + (m0 + sr) * sam, *bp = b + (n0 + sr) * sbn;
+    float ra[PT], rb[PT];
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int j = 0; j < PT; ++j) {
+            const int k = k0 + sk + j * (256 / GT);
+            ra[j] = (mok && k < ke) ? ap[k * sak] : 0.f;
+            rb[j] = (nok && k < ke) ? bp[k * sbk] : 0.f;
+        }
+    };
+    fetch(kb);
     for (int k0 = kb; k0 < ke; k0 += GK) {
-        for (int i = threadIdx.x; i < GK * GT; i += 256) {
-            const int kk = i / GT, r = i % GT;
-            const int m = m0 + r, n = n0 + r, k = k0 + kk;
-            As[kk][r] = (m < M && k < ke) ? a[m * sam + k * sak] : 0.f;
-            Bs[kk][r] = (n < N && k < ke) ? b[k * sbk + n * sbn] : 0.f;
+#pragma unroll
+        for (int j = 0; j < PT; ++j) {
+            As[sk + j * (256 / GT)][sr] = ra[j];
+            Bs[sk + j * (256 / GT)][sr] = rb[j];
         }
         __syncthreads();
+        if (k0 + GK < ke) fetch(k0 + GK);
         if (rsum) rsacc = rowsum_step(As, rsacc);
 #pragma unroll
         for (int kk = 0; kk < GK; kk += 4) {
