@@ -174,14 +174,29 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(int M, int N, int K, con
             }
 }
 
+// sum_{z < Z} p[z * stride], added in z order (deterministic) with 8 loads in flight
+MPCD_DEV float sum_slices(const float *p, int64_t stride, int Z)
+{
+    float acc = 0.f;
+    int z = 0;
+    for (; z + 8 <= Z; z += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = p[(z + u) * stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; z < Z; ++z) acc += p[z * stride];
+    return acc;
+}
+
 // C[m][n] = beta * C + sum_z part[z][m][n] (+ bias[n])
 __global__ void splitk_reduce_kernel(int M, int N, int Z, const float *part, float *c, int64_t ldc, float beta,
                                      const float *bias)
 {
     const int64_t n = (int64_t)M * N;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        float acc = 0.f;
-        for (int z = 0; z < Z; ++z) acc += part[z * n + i];
+        float acc = sum_slices(part + i, n, Z);
         const int m = (int)(i / N), j = (int)(i - (int64_t)m * N);
         if (bias) acc += bias[j];
         float *p = c + m * ldc + j;
@@ -218,9 +233,7 @@ __global__ void colsum_reduce_kernel(int N, int Z, const float *part, float *db)
 {
     const int n = blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= N) return;
-    float acc = 0.f;
-    for (int z = 0; z < Z; ++z) acc += part[(int64_t)z * N + n];
-    db[n] += acc;
+    db[n] += sum_slices(part + n, N, Z);
 }
 
 MPCD_DEV float softplus(float x) { return log1pf(expf(x)); }  // as torch's Mish kernels (no threshold)
