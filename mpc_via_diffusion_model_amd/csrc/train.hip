@@ -682,6 +682,8 @@ struct Trainer {
     };
     std::vector<UBuf> U;
     std::vector<float *> ucol, ustat, upart;
+    float *ugrad = nullptr;  // every trunk gradient buffer in one slab: one memset per step
+    int64_t ugrad_n = 0;
     int tL(int t) const { return sp.ut[t].L; }
     int tC(int t) const { return sp.ut[t].C; }
 
@@ -691,13 +693,21 @@ struct Trainer {
         U.assign(nt, UBuf{});
         U[UT_XNOISY] = {A.xn, nullptr};
         U[UT_MC] = {A.mc, A.dmc};
+        std::vector<int64_t> goff(nt, 0);
+        ugrad_n = 0;
+        for (int t = 2; t < nt; ++t) {
+            if (t == sp.u_out) continue;
+            goff[t] = ugrad_n;
+            ugrad_n += (B * tL(t) * tC(t) + 63) / 64 * 64;
+        }
+        if (!(ugrad = alloc(ugrad_n))) return -1;
         for (int t = 2; t < nt; ++t) {
             if (t == sp.u_out) {
                 U[t] = {A.out, A.dout};
                 continue;
             }
             U[t].v = alloc(B * tL(t) * tC(t));
-            U[t].g = alloc(B * tL(t) * tC(t));
+            U[t].g = ugrad + goff[t];
         }
         ucol.assign(no, nullptr);
         ustat = upart = ucol;
@@ -854,7 +864,7 @@ struct Trainer {
             A.dy[j] = alloc(B * co);
             A.dh[j] = alloc(B * co);
         }
-        if (sp.unet) reserve_unet(B);
+        if (sp.unet && reserve_unet(B) != 0) return -1;
         for (float *b : bufs)
             if (!b) return -1;
         cap = B;
@@ -942,9 +952,7 @@ struct Trainer {
             if ((e = hipMemsetAsync(A.dy[j], 0, (size_t)B * sp.blocks[j].co * 4, st)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(A.dmc, 0, (size_t)B * W * 4, st)) != hipSuccess) return e;
         if (sp.unet) {
-            for (int t = 2; t < (int)U.size(); ++t)
-                if (t != sp.u_out && (e = hipMemsetAsync(U[t].g, 0, (size_t)B * tL(t) * tC(t) * 4, st)) != hipSuccess)
-                    return e;
+            if ((e = hipMemsetAsync(ugrad, 0, (size_t)ugrad_n * 4, st)) != hipSuccess) return e;
             if ((e = unet_bwd(B)) != hipSuccess) return e;
         } else {
             if ((e = lin_bwd(B, A.f1, sp.base, sp.f2, 0, sp.base, A.dout, A.tmp, 0.f, true)) != hipSuccess) return e;  // d f1
