@@ -65,14 +65,18 @@ struct LoopGroup {
     std::condition_variable cv;
     int arrived = 0;
     uint64_t gen = 0;
+    bool broken = false;  // a member timed out: the phases can no longer pair up, every later call fails
     std::vector<const void *> src;
     std::vector<hipEvent_t> ready, copied;  // owned by the member ranks
     std::vector<bool> joined;
 
-    // every member thread must call; false on timeout (a peer that never arrives)
+    // every member thread must call; false on timeout (a peer that never arrives) and on every call after
+    // one: a timed-out member has left the generation its arrival counted in, so a late peer would release
+    // it and the next collective would pair mismatched phases (stale buffers) instead of failing
     bool barrier()
     {
         std::unique_lock<std::mutex> lk(mu);
+        if (broken) return false;
         const uint64_t g = gen;
         if (++arrived == n) {
             arrived = 0;
@@ -80,7 +84,10 @@ struct LoopGroup {
             cv.notify_all();
             return true;
         }
-        return cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g; });
+        if (cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g || broken; }) && !broken) return true;
+        broken = true;
+        cv.notify_all();
+        return false;
     }
 };
 
@@ -127,7 +134,8 @@ struct LoopbackComm final : Comm {
     int rendezvous(std::string &err)
     {
         if (!g->barrier()) {
-            err = "loopback communicator: a peer rank did not reach the collective within 120 s";
+            err = "loopback communicator: a peer rank did not reach a collective within 120 s (the group is "
+                  "unusable from then on)";
             return MPCD_ESTATE;
         }
         return MPCD_OK;

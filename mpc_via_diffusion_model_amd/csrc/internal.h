@@ -28,6 +28,20 @@ void launch_ctx_prologue(const float *ctx, int64_t n_rows, int ctx_dim, const Co
 hipError_t launch_philox_noise(uint64_t seed, int64_t goff, int64_t n, int n_slices, int flat, float *out,
                                hipStream_t stream);
 
+// Thread-safe launch state (several host threads may launch, e.g. the loopback communicator's ranks):
+// allow_max_lds<&kernel>() raises the kernel's dynamic-LDS cap to 160 KiB exactly once per kernel (one
+// instantiation per kernel address; a C++11 function-local static initialiser runs once, whichever
+// thread gets there first, and the others wait for it); device_cu_count() is the compute-unit count of
+// the CURRENT device, cached per device.
+template <auto Kernel>
+inline hipError_t allow_max_lds()
+{
+    static const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(Kernel),
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return e;
+}
+int device_cu_count();
+
 struct MlpSampleArgs {
     const float *wpack;      // packed linear layers (see mlp_sampler.hip)
     const StepPlan *plan;    // [S]

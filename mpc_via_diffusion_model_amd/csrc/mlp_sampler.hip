@@ -532,13 +532,7 @@ hipError_t launch_impl(const MlpSampleArgs &a, hipStream_t stream)
     using L = Lds<D0, MlpKernel<D0, SMODE, CTX>::NB>;
     static_assert(sizeof(float) * L::total(CTX) <= 160 * 1024, "LDS budget (160 KiB per CU)");
     const size_t lds_bytes = sizeof(float) * L::total(CTX);
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&mlp_sample_kernel<D0, SMODE, CTX>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    if (hipError_t e = allow_max_lds<&mlp_sample_kernel<D0, SMODE, CTX>>(); e != hipSuccess) return e;
     const int64_t blocks = (a.batch + L::CPW - 1) / L::CPW;
     hipLaunchKernelGGL((mlp_sample_kernel<D0, SMODE, CTX>), dim3((unsigned)blocks), dim3(THREADS), lds_bytes, stream, a);
     return hipGetLastError();

@@ -748,13 +748,7 @@ hipError_t launch_x3_r(const MlpSampleArgs &a, hipStream_t stream)
     using L = Lds3<D0, MlpX3<D0, SMODE, CTX, R, W>::NB, R>;
     static_assert(W == 8 || 2 * L::total <= 160 * 1024, "two 4-wave workgroups per CU");
     static_assert(L::total <= 160 * 1024, "LDS budget (160 KiB per CU)");
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&mlp_x3_kernel<D0, SMODE, CTX, R, W>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    if (hipError_t e = allow_max_lds<&mlp_x3_kernel<D0, SMODE, CTX, R, W>>(); e != hipSuccess) return e;
     const int64_t blocks = (a.batch + L::CPW - 1) / L::CPW;
     hipLaunchKernelGGL((mlp_x3_kernel<D0, SMODE, CTX, R, W>), dim3((unsigned)blocks), dim3(64 * W), (size_t)L::total, stream,
                        a);
@@ -775,13 +769,7 @@ int mlp_x3_layout(int64_t batch, int nb)
         return !strcmp(e, "32x8") ? (int)LAYOUT_32x8 : !strcmp(e, "16x8") ? (int)LAYOUT_16x8 : !strcmp(e, "16x4") ? (int)LAYOUT_16x4 : -1;
     }();
     if (forced >= 0) return forced;
-    static int n_cu = 0;
-    if (!n_cu) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            n_cu = 256;
-    }
+    const int n_cu = device_cu_count();
     return (batch * nb + 31) / 32 < n_cu ? LAYOUT_16x8 : LAYOUT_32x8;
 }
 

@@ -8,6 +8,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -37,6 +38,19 @@ hipError_t launch_control_step(const mpcd_system_desc &d, double *x_dev, int64_t
 hipError_t launch_argmin(const double *cost, int64_t n, int64_t offset, mpcd_best *best, hipStream_t stream);
 hipError_t launch_winner_row(const mpcd_best *best, int64_t lo, int64_t n_local, const float *rows, int row_len,
                              float *out, hipStream_t stream);
+
+int device_cu_count()
+{
+    constexpr int kMaxDev = 64;
+    static std::atomic<int> cu[kMaxDev];  // 0 = not yet queried (zero-initialised: static storage)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 256;
+    int n = cu[dev].load(std::memory_order_relaxed);
+    if (n > 0) return n;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cu[dev].store(n, std::memory_order_relaxed);
+    return n;
+}
 
 namespace {
 
@@ -1104,6 +1118,7 @@ int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, fl
 struct mpcd_trainer {
     Trainer *t = nullptr;
     int64_t n_params = 0;
+    int device = 0;  // the device current at mpcd_trainer_create: owns every buffer; each call switches to it
 };
 
 int mpcd_trainer_create(const mpcd_net_desc *desc, const float *params, size_t n_floats, const mpcd_train_cfg *cfg,
@@ -1253,9 +1268,11 @@ int mpcd_trainer_create(const mpcd_net_desc *desc, const float *params, size_t n
     std::copy(sqrt_alphas_cumprod, sqrt_alphas_cumprod + n_steps, sched.begin());
     std::copy(sqrt_one_minus_alphas_cumprod, sqrt_one_minus_alphas_cumprod + n_steps, sched.begin() + n_steps);
     std::string why;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
     Trainer *t = trainer_new(sp, params, sched.data(), &why);
     if (!t) return fail(MPCD_ENOMEM, "%s", why.c_str());
-    *out = new mpcd_trainer{t, o};
+    *out = new mpcd_trainer{t, o, dev};
     return MPCD_OK;
 }
 
@@ -1264,6 +1281,7 @@ int mpcd_trainer_step(mpcd_trainer *tr, const float *x0, const float *context, c
 {
     if (!tr || !x0 || !context || !t || !noise || !context_mask || !loss || batch < 1)
         return fail(MPCD_EINVAL, "mpcd_trainer_step: null argument or empty batch");
+    HIP_TRY(hipSetDevice(tr->device));
     TrainBatch b{x0, context, noise, context_mask, t, batch, hip_stream};
     std::string why;
     const int r = trainer_step(tr->t, b, update != 0, loss, &why);
@@ -1275,6 +1293,7 @@ int mpcd_trainer_step(mpcd_trainer *tr, const float *x0, const float *context, c
 int mpcd_trainer_params(mpcd_trainer *tr, int32_t which, float *host_out, size_t n_floats)
 {
     if (!tr || !host_out || which < 0 || which > 4) return fail(MPCD_EINVAL, "mpcd_trainer_params: bad argument");
+    HIP_TRY(hipSetDevice(tr->device));
     const int r = trainer_read(tr->t, which, host_out, n_floats);
     if (r == -1) return fail(MPCD_EINVAL, "mpcd_trainer_params: %zu floats, the net has %lld", n_floats, (long long)tr->n_params);
     if (r != 0) return fail(MPCD_EHIP, "mpcd_trainer_params: copy failed");
@@ -1284,6 +1303,7 @@ int mpcd_trainer_params(mpcd_trainer *tr, int32_t which, float *host_out, size_t
 int mpcd_trainer_comm_init(mpcd_trainer *tr, int32_t nranks, int32_t rank, const void *id_in)
 {
     if (!tr || !id_in || nranks < 1 || rank < 0 || rank >= nranks) return fail(MPCD_EINVAL, "bad comm arguments");
+    HIP_TRY(hipSetDevice(tr->device));
     std::string e;
     Comm *c = nullptr;
     if (int rc = comm_create_rccl(nranks, rank, id_in, &c, e)) return fail(rc, "%s", e.c_str());
@@ -1297,6 +1317,7 @@ int mpcd_trainer_comm_init(mpcd_trainer *tr, int32_t nranks, int32_t rank, const
 int mpcd_trainer_comm_init_loopback(mpcd_trainer *tr, int32_t nranks, int32_t rank, uint64_t group_key)
 {
     if (!tr || nranks < 1 || rank < 0 || rank >= nranks) return fail(MPCD_EINVAL, "bad comm arguments");
+    HIP_TRY(hipSetDevice(tr->device));
     std::string e;
     Comm *c = nullptr;
     if (int rc = comm_create_loopback(nranks, rank, group_key, &c, e)) return fail(rc, "%s", e.c_str());
@@ -1310,6 +1331,7 @@ int mpcd_trainer_comm_init_loopback(mpcd_trainer *tr, int32_t nranks, int32_t ra
 void mpcd_trainer_destroy(mpcd_trainer *tr)
 {
     if (!tr) return;
+    (void)hipSetDevice(tr->device);
     trainer_free(tr->t);
     delete tr;
 }

@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -852,7 +853,9 @@ struct Trainer {
         A.dmc = alloc(B * W);
         A.dcemb = alloc(B * W);
         A.dq1 = alloc(B * 128);
-        A.tmp = alloc(B * 256);
+        int wtmp = std::max(256, sp.base);  // widest backward scratch: d(h1) / d(a1) of every block, d(f1)
+        for (int j = 0; j < nb; ++j) wtmp = std::max(wtmp, sp.blocks[j].co);
+        A.tmp = alloc(B * wtmp);
         A.a1.assign(nb, nullptr);
         A.h1 = A.s = A.y = A.dy = A.dh = A.a1;
         for (int j = 0; j < nb; ++j) {
@@ -1018,6 +1021,7 @@ Trainer *trainer_new(const TrainSpec &sp, const float *params_host, const float 
 int trainer_step(Trainer *t, const TrainBatch &b, bool update, double *loss, std::string *why)
 {
     t->st = (hipStream_t)b.stream;
+    t->comm_err.clear();  // a previous step's all-reduce failure must not label this step's errors
     if (t->reserve(b.batch) != 0) {
         if (why) *why = "trainer: activation buffers";
         return -1;

@@ -618,13 +618,7 @@ int rows_per_wg(int kind, int lin, int lout, int cinp, int coutp, int halo, size
 template <int KIND, int EPI>
 hipError_t launch_conv(const ConvK &k, size_t lds, hipStream_t st)
 {
-    static bool set = false;
-    if (!set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&conv_kernel<KIND, EPI>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        set = true;
-    }
+    if (hipError_t e = allow_max_lds<&conv_kernel<KIND, EPI>>(); e != hipSuccess) return e;
     const int64_t blocks = (k.rows + k.rb - 1) / k.rb;
     hipLaunchKernelGGL((conv_kernel<KIND, EPI>), dim3((unsigned)blocks), dim3(CT), lds, st, k);
     return hipGetLastError();

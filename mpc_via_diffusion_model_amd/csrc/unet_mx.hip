@@ -751,7 +751,28 @@ struct Tile {
 constexpr Tile kTiles3[] = {{2, 4}, {1, 8}, {1, 4}};
 constexpr Tile kTiles1[] = {{4, 8}, {2, 8}, {2, 4}, {1, 8}, {1, 4}};
 
-int g_n_cu = 0;  // compute units of the device (persistent grids)
+// Workgroups of a kernel that fit one CU at `lds` bytes of dynamic LDS (occupancy query, cached per
+// (kernel, lds) under a mutex: launches may come from several host threads).
+hipError_t resident_per_cu(const void *fn, size_t lds, int &out)
+{
+    static std::mutex mu;
+    static std::map<std::pair<const void *, size_t>, int> cache;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = cache.find({fn, lds});
+        if (it != cache.end()) {
+            out = it->second;
+            return hipSuccess;
+        }
+    }
+    int n = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, MT, lds);
+    if (e != hipSuccess) return e;
+    out = std::max(n, 1);
+    std::lock_guard<std::mutex> g(mu);
+    cache[{fn, lds}] = out;
+    return hipSuccess;
+}
 
 // LDS bytes of the pre-norm output tile (rows x (coutp + pad)), as the kernel lays it out
 size_t tile_bytes(int planes, size_t rows, int coutp)
@@ -763,56 +784,27 @@ template <int KIND, int P, int NN, int NC, bool PERS, int NPH = 1>
 hipError_t launch_one(const ConvMK2 &k2, size_t lds, hipStream_t st)
 {
     const ConvMK &k = k2.ph[0];
-    auto *fn = reinterpret_cast<const void *>(conv_kernel_ptr<KIND, P, NN, NC, PERS, NPH>());
-    static bool set = false;
-    static int resident = 0;  // workgroups per CU at this kernel's registers and the LDS of its first use
-    static size_t resident_lds = 0;
-    if (!set) {
-        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        set = true;
-    }
+    constexpr auto kfn = conv_kernel_ptr<KIND, P, NN, NC, PERS, NPH>();
+    auto *fn = reinterpret_cast<const void *>(kfn);
+    if (hipError_t e = allow_max_lds<kfn>(); e != hipSuccess) return e;
     int64_t blocks = (k.rows + k.rb - 1) / k.rb;
+    int resident = 1;  // workgroups per CU at this kernel's registers and this launch's LDS
+    const int n_cu = device_cu_count();
     if (PERS) {
-        if (resident_lds != lds) {
-            int n = 0;
-            hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, MT, lds);
-            if (e != hipSuccess) return e;
-            resident = std::max(n, 1);
-            resident_lds = lds;
-        }
-        if (!g_n_cu) {
-            int dev = 0;
-            hipError_t e = hipGetDevice(&dev);
-            if (e == hipSuccess) e = hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-            if (e != hipSuccess) return e;
-        }
-        blocks = std::min<int64_t>(blocks, (int64_t)resident * g_n_cu);
+        if (hipError_t e = resident_per_cu(fn, lds, resident); e != hipSuccess) return e;
+        blocks = std::min<int64_t>(blocks, (int64_t)resident * n_cu);
     }
     static const int stag = [] {  // experiment knob: first-generation stagger units per resident slot
         const char *e = getenv("MPCD_UNET_STAGGER");
         return e ? atoi(e) : 0;
     }();
     if (!PERS && stag > 0) {
-        if (resident_lds != lds) {
-            int n = 0;
-            hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, MT, lds);
-            if (e != hipSuccess) return e;
-            resident = std::max(n, 1);
-            resident_lds = lds;
-        }
-        if (!g_n_cu) {
-            int dev = 0;
-            hipError_t e = hipGetDevice(&dev);
-            if (e == hipSuccess) e = hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-            if (e != hipSuccess) return e;
-        }
-        if (resident > 1 && blocks > (int64_t)resident * g_n_cu) {
+        if (hipError_t e = resident_per_cu(fn, lds, resident); e != hipSuccess) return e;
+        if (resident > 1 && blocks > (int64_t)resident * n_cu) {
             ConvMK2 k3 = k2;
             k3.ph[0].stag_units = stag;
-            k3.ph[0].stag_ncu = g_n_cu;
+            k3.ph[0].stag_ncu = n_cu;
             k3.ph[0].stag_slots = resident;
-            auto kfn = conv_kernel_ptr<KIND, P, NN, NC, PERS, NPH>();
             hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(MT), lds, st, k3);
             return hipGetLastError();
         }
@@ -821,7 +813,6 @@ hipError_t launch_one(const ConvMK2 &k2, size_t lds, hipStream_t st)
         const char *e = getenv("MPCD_UNET_LDS_PAD");
         return e ? (size_t)atol(e) : (size_t)0;
     }();
-    auto kfn = conv_kernel_ptr<KIND, P, NN, NC, PERS, NPH>();
     hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(MT),
                        std::min(lds + lds_pad, (size_t)160 * 1024), st, k2);
     return hipGetLastError();

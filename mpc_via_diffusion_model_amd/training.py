@@ -38,10 +38,13 @@ class DiffusionTrainer:
         sac = self.tables["sqrt_alphas_cumprod"].to(torch.float32).contiguous()
         s1m = self.tables["sqrt_one_minus_alphas_cumprod"].to(torch.float32).contiguous()
         self._tr = ctypes.c_void_p()
-        N.check(self._lib.mpcd_trainer_create(ctypes.byref(self._desc), ctypes.c_void_p(blob.data_ptr()), self.n_params,
-                                              ctypes.byref(cfg), ctypes.c_void_p(sac.data_ptr()),
-                                              ctypes.c_void_p(s1m.data_ptr()), self.n_steps, ctypes.byref(self._tr)),
-                "mpcd_trainer_create")
+        # the trainer's buffers live on the device current at mpcd_trainer_create (every later mpcd_trainer_*
+        # call switches back to it)
+        with torch.cuda.device(self.device):
+            N.check(self._lib.mpcd_trainer_create(ctypes.byref(self._desc), ctypes.c_void_p(blob.data_ptr()), self.n_params,
+                                                  ctypes.byref(cfg), ctypes.c_void_p(sac.data_ptr()),
+                                                  ctypes.c_void_p(s1m.data_ptr()), self.n_steps, ctypes.byref(self._tr)),
+                    "mpcd_trainer_create")
 
     def data_parallel(self, group=None, loopback=None):
         """Average gradients over ranks before each Adam step (DistributedDataParallel's rule) through an RCCL
@@ -80,7 +83,10 @@ class DiffusionTrainer:
 
     # ---------------------------------------------------------------- the reference's random draws
     def draw(self, batch, shape, generator=None):
-        """t, noise, context_mask in p_losses' order (loss(): randint; p_losses: randn_like, rand, bernoulli)."""
+        """t, noise, context_mask in p_losses' order (loss(): randint; p_losses: randn_like, rand, bernoulli), all
+        from torch's CPU generator. This is the reference's stream only for a batch on the CPU: for a CUDA batch
+        the reference draws randint / randn_like on x.device (diffusion_model_base.py:435,466) from the CUDA
+        generator and only rand / bernoulli on the CPU; pass t / noise explicitly to reproduce such a run."""
         t = torch.randint(0, self.n_steps, (batch,), generator=generator).long()
         noise = torch.randn(shape, generator=generator)
         mask_shape = torch.rand(batch, 1, generator=generator)
