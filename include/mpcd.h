@@ -340,6 +340,13 @@ int mpcd_unet_force_tiling(int32_t conv_pick, int32_t block_pick);
  * 16x8 when 32-row workgroups would leave CUs idle); 0 = 32x8; 1 = 16x8; 2 = 16x4 (two 4-wave workgroups per
  * CU where their LDS fits, else 16x8). All layouts compute the same sums in the same order. */
 int mpcd_mlp_force_layout(int32_t layout);
+/* U-Net execution form, process-wide. The whole-network form (csrc/unet_fused.hip: every conv of one denoise
+ * step in ONE launch, a workgroup per few candidates, activations in LDS) covers the CFG samplers and the
+ * two-branch eps of ConditionedTemporalUnet(base 32, dim_mults (1, 2, 4)) at H = 32 / 64 with the MPCD_F32X3
+ * or MPCD_F16 numerics; everything else runs layer by layer (one launch per conv). 0 = automatic (the fused
+ * form where it applies; env MPCD_UNET_FUSED=0 turns it off), 1 = layer by layer, 2 = fused (a sample / eps
+ * call it does not cover returns MPCD_EUNSUP). */
+int mpcd_unet_force_path(int32_t path);
 #define MPCD_UNET_MAX_CONV_TILINGS 12   /* 6 rows-per-workgroup values x {tiled, persistent} */
 #define MPCD_UNET_MAX_BLOCK_TILINGS 6
 

@@ -8,6 +8,6 @@ Compute is in libmpcd.so (hand-written HIP for gfx950, built by ``python -m
 mpc_via_diffusion_model_amd.build``); see DESIGN.md and include/mpcd.h.
 """
 from . import systems
-from .planner import ClosedLoopResult, DiffusionMPC, MPCResult, NetSpec, force_unet_tiling, philox_noise
+from .planner import ClosedLoopResult, DiffusionMPC, MPCResult, NetSpec, force_unet_path, force_unet_tiling, philox_noise
 
-__all__ = ["ClosedLoopResult", "DiffusionMPC", "MPCResult", "NetSpec", "force_unet_tiling", "philox_noise", "systems"]
+__all__ = ["ClosedLoopResult", "DiffusionMPC", "MPCResult", "NetSpec", "force_unet_path", "force_unet_tiling", "philox_noise", "systems"]

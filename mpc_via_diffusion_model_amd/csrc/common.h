@@ -96,3 +96,51 @@ enum { PLAN_NOISE = 1, PLAN_FINAL = 2 };
 enum { MODE_DDPM_CFG = 0, MODE_DDIM_CFG = 1, MODE_DDIM = 2, MODE_EPS = 3, MODE_EPS1 = 4 };
 // MODE_EPS / MODE_EPS1: one net forward at plan[0].t on x = noise[0]; eps of the context branch ->
 // x_out, of the masked branch -> chain (MODE_EPS, CFG net) or just x_out (MODE_EPS1, 3-arg net).
+
+// One element quad of a denoise step (p_mean_variance_CFG, diffusion_model_base.py:164-178, then
+// ddpm_cart_pole_sample_fn, sample_functions.py:17-44; the build-defined CFG-DDIM; the reference's
+// ddim_sample, :239-314) in the reference's op order. Every translation unit is compiled with
+// -ffp-contract=off, so no product is fused into an add. ec / eu: eps of the context / masked branch
+// (eu unused for MODE_DDIM); z: this step's noise (used when the plan adds noise).
+MPCD_DEV f32x4 denoise_update4(const StepPlan &sp, int mode, int clamp_x0, float wp1, float wf, const f32x4 &xv,
+                               const f32x4 &ec, const f32x4 &eu, const f32x4 &z)
+{
+    f32x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float xr = xv[r];
+        if (mode == MODE_DDPM_CFG) {
+            const float x0c = sp.a * xr - sp.b * ec[r];
+            const float x0u = sp.a * xr - sp.b * eu[r];
+            float x0 = wp1 * x0c - wf * x0u;
+            x0 = clamp1(x0);
+            const float mean = sp.c1 * x0 + sp.c2 * xr;
+            o[r] = (sp.flags & PLAN_NOISE) ? mean + sp.std * z[r] : mean;
+        } else if (mode == MODE_DDIM_CFG) {
+            float x0 = wp1 * (sp.a * xr - sp.b * ec[r]) - wf * (sp.a * xr - sp.b * eu[r]);
+            if (clamp_x0) x0 = clamp1(x0);
+            const float e = wp1 * ec[r] - wf * eu[r];
+            o[r] = (sp.flags & PLAN_FINAL) ? x0 : x0 * sp.sqan + sp.cn * e;
+        } else {
+            float x0 = sp.a * xr - sp.b * ec[r];
+            if (clamp_x0) x0 = clamp1(x0);
+            o[r] = (sp.flags & PLAN_FINAL) ? x0 : x0 * sp.sqan + sp.cn * ec[r];
+        }
+    }
+    return o;
+}
+
+// running chain |x| maximum of one element quad (bits of |x| as uint32: a NaN wins the integer max);
+// elements are copied to scalars first (a __builtin_bit_cast of a vector-element subscript compiled to
+// element 0 for every index)
+MPCD_DEV uint32_t absmax_bits4(uint32_t m, const f32x4 &a, const f32x4 &b)
+{
+    const float ae[4] = {a.x, a.y, a.z, a.w}, be[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t u = __builtin_bit_cast(uint32_t, ae[r]) & 0x7fffffffu;
+        const uint32_t v = __builtin_bit_cast(uint32_t, be[r]) & 0x7fffffffu;
+        m = max(m, max(u, v));
+    }
+    return m;
+}

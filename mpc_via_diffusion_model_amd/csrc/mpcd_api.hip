@@ -654,7 +654,7 @@ int mpcd_sample(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr)
         u.clamp_x0 = a->clamp_x0;
         u.wp1 = wp1;
         u.wf = wf;
-        size_t ws = unet_workspace_bytes(d, a->batch, cfg ? 2 : 1);
+        size_t ws = unet_workspace_bytes(d, c->unet, a->sampler, a->batch, cfg ? 2 : 1);
         if ((rc = c->unet_ws.ensure(ws))) return rc;
         u.workspace = c->unet_ws.p;
         rc = unet_sample(d, c->unet, u, st);
@@ -713,7 +713,7 @@ int mpcd_eps(mpcd_ctx *c, const float *x, int32_t t, const float *context, int32
         u.x_in = x;
         u.eps_cond = eps_cond;
         u.eps_uncond = eps_uncond;
-        if ((rc = c->unet_ws.ensure(unet_workspace_bytes(d, batch, cfg ? 2 : 1)))) return rc;
+        if ((rc = c->unet_ws.ensure(unet_workspace_bytes(d, c->unet, u.mode, batch, cfg ? 2 : 1)))) return rc;
         u.workspace = c->unet_ws.p;
         rc = unet_sample(d, c->unet, u, st);
         if (rc) return fail(rc, "unet eps: %s", unet_last_error());
@@ -756,6 +756,13 @@ int mpcd_unet_force_tiling(int32_t conv_pick, int32_t block_pick)
 {
     if (conv_pick < -1 || block_pick < -2) return fail(MPCD_EINVAL, "conv_pick >= -1, block_pick >= -2");
     unet_force_tiling(conv_pick, block_pick);
+    return MPCD_OK;
+}
+
+int mpcd_unet_force_path(int32_t path)
+{
+    if (path < 0 || path > 2) return fail(MPCD_EINVAL, "path 0 (auto), 1 (layer by layer) or 2 (fused)");
+    unet_force_path(path);
     return MPCD_OK;
 }
 

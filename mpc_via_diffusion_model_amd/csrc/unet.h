@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <functional>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -67,11 +68,17 @@ struct ConvMK {
     uint32_t *wgtrace;      // diagnostics (MPCD_UNET_WGTRACE): per workgroup {start, end, HW_ID, XCC_ID}
 };
 
+// Whole-network-per-workgroup form (unet_fused.hip): the op program and its LDS placement.
+struct UnetFusedPlan;
+void unet_fused_free(UnetFusedPlan *p);
+
 struct UnetWeights {
     bool ready = false;
     int n_layers = 0;
     int planes = 0;                 // 0: fp32 MFMA kernels (unet.hip); 3: split-bf16, 1: f16 (unet_mx.hip)
     std::vector<ConvLayer> layers;  // in execution order (see unet.hip build_plan)
+    std::shared_ptr<UnetFusedPlan> fused;  // null when the fused form does not cover the net
+    std::string fused_why;                 // why not (diagnostics)
 };
 
 struct UnetSampleArgs {
@@ -113,6 +120,30 @@ hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::
 // intermediate then stays in LDS and k1.out is not written). MPCD_UNET_FUSE=0/1 forces either form.
 hipError_t unet_launch_mx_rtb(int planes, ConvMK &k1, ConvMK &k2, hipStream_t st, std::string *why);
 
+// One denoise step of the fused form (unet_fused_step): x [B][H][d] is updated in place (or is the input of
+// MODE_EPS, whose eps of both branches go to eps_c / eps_u).
+struct UnetFusedStep {
+    float *x;
+    int64_t batch, goff;
+    int mode, clamp_x0, step, last;
+    const float *tp, *cp;  // tproj row of this step, cproj (or null)
+    int64_t cp_stride;
+    const StepPlan *plan;
+    float wp1, wf;
+    const float *noise;
+    uint64_t seed;
+    float *chain, *x_out;
+    uint32_t *amq;
+    float *eps_c, *eps_u;
+    void *scratch;  // unet_fused_scratch_bytes
+};
+UnetFusedPlan *unet_fused_prepare(const mpcd_net_desc &d, const UnetWeights &W, int rows_per_wg, std::string *why);
+size_t unet_fused_scratch_bytes(const UnetFusedPlan &pl, int64_t batch);
+int unet_fused_rows_per_wg(const UnetFusedPlan &pl);
+hipError_t unet_fused_step(const UnetFusedPlan &pl, const UnetFusedStep &s, hipStream_t st);
+// mpcd_unet_force_path: 0 = automatic, 1 = layer by layer, 2 = fused (error where it does not apply)
+void unet_force_path(int path);
+
 // mpcd_unet_force_tiling (include/mpcd.h)
 void unet_force_tiling(int conv, int block);
 
@@ -122,6 +153,6 @@ using TensorLookup = std::function<const float *(const char *)>;
 // Repacks conv weights into `pack` (device, grown as needed).
 int unet_prepare(const mpcd_net_desc &d, size_t n_tensors, const TensorLookup &dev, const TensorLookup &host,
                  UnetWeights &w, void *&pack, size_t &pack_bytes);
-size_t unet_workspace_bytes(const mpcd_net_desc &d, int64_t batch, int nb);
+size_t unet_workspace_bytes(const mpcd_net_desc &d, const UnetWeights &w, int mode, int64_t batch, int nb);
 int unet_sample(const mpcd_net_desc &d, const UnetWeights &w, const UnetSampleArgs &a, hipStream_t stream);
 const char *unet_last_error();

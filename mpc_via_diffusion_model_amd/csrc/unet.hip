@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -302,41 +303,9 @@ __global__ void update_kernel(float *x, const float *eps, int64_t batch, int fla
     if (mode == MODE_DDPM_CFG && (sp.flags & PLAN_NOISE))
         z = noise ? *reinterpret_cast<const f32x4 *>(noise + (size_t)(s + 1) * batch * flat + off)
                   : philox_normal4(seed, (uint64_t)(goff + b), (uint32_t)(s + 1), (uint32_t)qd);
-    f32x4 o;
-    for (int r = 0; r < 4; ++r) {
-        const float xr = xv[r];
-        if (mode == MODE_DDPM_CFG) {
-            const float x0c = sp.a * xr - sp.b * ec[r];
-            const float x0u = sp.a * xr - sp.b * eu[r];
-            float x0 = wp1 * x0c - wf * x0u;
-            x0 = clamp1(x0);
-            const float mean = sp.c1 * x0 + sp.c2 * xr;
-            o[r] = (sp.flags & PLAN_NOISE) ? mean + sp.std * z[r] : mean;
-        } else if (mode == MODE_DDIM_CFG) {
-            float x0 = wp1 * (sp.a * xr - sp.b * ec[r]) - wf * (sp.a * xr - sp.b * eu[r]);
-            if (clamp_x0) x0 = clamp1(x0);
-            const float e = wp1 * ec[r] - wf * eu[r];
-            o[r] = (sp.flags & PLAN_FINAL) ? x0 : x0 * sp.sqan + sp.cn * e;
-        } else {
-            float x0 = sp.a * xr - sp.b * ec[r];
-            if (clamp_x0) x0 = clamp1(x0);
-            o[r] = (sp.flags & PLAN_FINAL) ? x0 : x0 * sp.sqan + sp.cn * ec[r];
-        }
-    }
+    const f32x4 o = denoise_update4(sp, mode, clamp_x0, wp1, wf, xv, ec, eu, z);
     *reinterpret_cast<f32x4 *>(x + off) = o;
-    if (amq) {  // running chain |x| maximum of this quad: x read (x_T at s = 0, then each slice) and written
-        // (elements copied to scalars first: a __builtin_bit_cast of a vector-element subscript compiled to
-        // element 0 for every r)
-        uint32_t m = s == 0 ? 0u : amq[i];
-        const float xe[4] = {xv.x, xv.y, xv.z, xv.w}, oe[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint32_t a = __builtin_bit_cast(uint32_t, xe[r]) & 0x7fffffffu;
-            const uint32_t b = __builtin_bit_cast(uint32_t, oe[r]) & 0x7fffffffu;
-            m = max(m, max(a, b));
-        }
-        amq[i] = m;
-    }
+    if (amq) amq[i] = absmax_bits4(s == 0 ? 0u : amq[i], xv, o);  // running chain |x| maximum of this quad
     if (chain) *reinterpret_cast<f32x4 *>(chain + (size_t)(s + 1) * batch * flat + off) = o;
     if (last && x_out != x) *reinterpret_cast<f32x4 *>(x_out + off) = o;
 }
@@ -533,6 +502,9 @@ int unet_prepare(const mpcd_net_desc &d, size_t, const TensorLookup &dev, const 
     W.planes = planes;
     W.n_layers = (int)W.layers.size();
     W.ready = true;
+    W.fused.reset();
+    W.fused_why.clear();
+    if (UnetFusedPlan *fp = unet_fused_prepare(d, W, 0, &W.fused_why)) W.fused.reset(fp, unet_fused_free);
     return MPCD_OK;
 }
 
@@ -827,16 +799,97 @@ int forward(Ctx &c, const Dims &m, Buffers &B, const float *x, int64_t x_rows)
 
 }  // namespace
 
-size_t unet_workspace_bytes(const mpcd_net_desc &d, int64_t batch, int nb)
+namespace {
+std::atomic<int> g_unet_path{0};  // mpcd_unet_force_path
+
+// the fused form runs the CFG samplers and the two-branch eps of a ConditionedTemporalUnet it covers;
+// MPCD_UNET_FUSED=0 turns it off (the layer-by-layer path then runs everything)
+bool use_fused(const UnetWeights &W, int mode)
+{
+    static const bool env_off = [] {
+        const char *e = getenv("MPCD_UNET_FUSED");
+        return e && e[0] == '0';
+    }();
+    const int path = g_unet_path.load();
+    if (!W.fused || path == 1 || (env_off && path != 2)) return false;
+    return mode == MODE_DDPM_CFG || mode == MODE_DDIM_CFG || mode == MODE_EPS;
+}
+}  // namespace
+
+void unet_force_path(int path) { g_unet_path.store(path); }
+
+size_t unet_workspace_bytes(const mpcd_net_desc &d, const UnetWeights &W, int mode, int64_t batch, int nb)
 {
     const Dims m = dims_of(d);
     // + the sampler state x [B][H][d] and the per-quad chain |x| maxima [B][H*d/4]
-    return sizeof(float) * (ws_floats(m, batch * nb) + (size_t)batch * m.H * m.d + (size_t)batch * (m.H * m.d / 4 + 1));
+    const size_t state = sizeof(float) * ((size_t)batch * m.H * m.d + (size_t)batch * (m.H * m.d / 4 + 1));
+    if (use_fused(W, mode)) return state + 256 + unet_fused_scratch_bytes(*W.fused, batch);
+    return sizeof(float) * ws_floats(m, batch * nb) + state;
 }
+
+namespace {
+// the whole net + the update of one denoise step per launch (unet_fused.hip)
+int sample_fused(const mpcd_net_desc &d, const UnetWeights &W, const UnetSampleArgs &a, hipStream_t st)
+{
+    const UnetFusedPlan &pl = *W.fused;
+    const int flat = d.horizon * d.state_dim;
+    float *xs = static_cast<float *>(a.workspace);
+    uint32_t *amq = a.chain_absmax ? reinterpret_cast<uint32_t *>(xs + (size_t)a.batch * flat) : nullptr;
+    char *scratch = reinterpret_cast<char *>(xs) +
+                    ((sizeof(float) * ((size_t)a.batch * flat + (size_t)a.batch * (flat / 4 + 1)) + 255) / 256 * 256);
+    UnetFusedStep f{};
+    f.batch = a.batch;
+    f.goff = a.global_offset;
+    f.mode = a.mode;
+    f.clamp_x0 = a.clamp_x0;
+    f.cp = a.cproj;
+    f.cp_stride = a.cproj_stride;
+    f.plan = a.plan;
+    f.wp1 = a.wp1;
+    f.wf = a.wf;
+    f.noise = a.noise;
+    f.seed = a.seed;
+    f.chain = a.chain;
+    f.x_out = a.x_out;
+    f.amq = amq;
+    f.scratch = scratch;
+    if (a.mode == MODE_EPS) {
+        f.x = const_cast<float *>(a.x_in);  // read only in MODE_EPS
+        f.tp = a.tproj;
+        f.eps_c = a.eps_cond;
+        f.eps_u = a.eps_uncond;
+        f.chain = f.x_out = nullptr;
+        f.amq = nullptr;
+        hipError_t e = unet_fused_step(pl, f, st);
+        return e == hipSuccess ? MPCD_OK : uerr(MPCD_EHIP, std::string("fused U-Net: ") + hipGetErrorString(e));
+    }
+    const int threads = 256;
+    const unsigned g1 = (unsigned)((a.batch * (flat / 4) + threads - 1) / threads);
+    hipLaunchKernelGGL(init_x_kernel, dim3(g1), dim3(threads), 0, st, xs, a.batch, flat, a.noise, a.seed,
+                       a.global_offset, a.chain);
+    f.x = xs;
+    for (int s = 0; s < a.n_steps; ++s) {
+        f.tp = a.tproj + (size_t)s * a.cond_total;
+        f.step = s;
+        f.last = s == a.n_steps - 1 ? 1 : 0;
+        hipError_t e = unet_fused_step(pl, f, st);
+        if (e != hipSuccess) return uerr(MPCD_EHIP, std::string("fused U-Net: ") + hipGetErrorString(e));
+    }
+    if (amq)
+        hipLaunchKernelGGL(chain_absmax_kernel, dim3((unsigned)((a.batch + 255) / 256)), dim3(256), 0, st, amq, a.batch,
+                           flat / 4, a.chain_absmax);
+    if (hipGetLastError() != hipSuccess) return uerr(MPCD_EHIP, "fused U-Net: update launch");
+    return MPCD_OK;
+}
+}  // namespace
 
 int unet_sample(const mpcd_net_desc &d, const UnetWeights &W, const UnetSampleArgs &a, hipStream_t st)
 {
     if (!W.ready) return uerr(MPCD_ESTATE, "UNet weights not prepared");
+    if (g_unet_path.load() == 2 && !use_fused(W, a.mode))
+        return uerr(MPCD_EUNSUP, "fused U-Net forced but not applicable: " +
+                                     (W.fused ? std::string("sampler mode") : W.fused_why));
+    if (use_fused(W, a.mode)) return sample_fused(d, W, a, st);
     const Dims m = dims_of(d);
     const bool eps_mode = a.mode == MODE_EPS || a.mode == MODE_EPS1;
     const int nb = (a.mode == MODE_DDIM || a.mode == MODE_EPS1) ? 1 : 2;

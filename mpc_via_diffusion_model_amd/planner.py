@@ -50,6 +50,15 @@ def force_unet_tiling(conv=-1, block=-1):
     N.check(N.lib().mpcd_unet_force_tiling(int(conv), int(block)), "mpcd_unet_force_tiling")
 
 
+UNET_PATHS = {"auto": 0, "layered": 1, "fused": 2}
+
+
+def force_unet_path(path="auto"):
+    """Process-wide U-Net execution form (mpcd_unet_force_path): "auto" (the whole-network fused launch where
+    it applies), "layered" (one launch per conv) or "fused" (error where it does not apply)."""
+    N.check(N.lib().mpcd_unet_force_path(UNET_PATHS[path]), "mpcd_unet_force_path")
+
+
 MLP_LAYOUTS = {"auto": -1, "32x8": 0, "16x8": 1, "16x4": 2}
 
 

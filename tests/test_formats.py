@@ -84,3 +84,18 @@ def test_inference_dump_layout(tmp_path):
     assert r["u_diffusion"].shape == (1, T) and r["u_horizon_diffusion"].shape == (T, H)
     assert r["x_diffusion_horizon"].shape == (T, H + 1, 5)
     np.testing.assert_array_equal(r["u_diffusion"][0], np.round(u[:, 0], 4))
+
+
+@pytest.mark.parametrize("name", ["lmpc_2406400_1000000", "lmpc_420000_noisy_230000"])
+def test_infer_spec_lmpc_checkpoints(name):
+    """The two CartPole-LMPC trained models (trained_models/2406400_models/1000000,
+    420000_models_with_noisy_data/230000; fixtures by tests/golden/make_lmpc_ckpts.py): d=1, C=4, H=32."""
+    from safetensors.torch import load_file
+    args = yaml.safe_load(open(os.path.join(HERE, "golden", f"{name}_args.yaml")))
+    sd = load_file(os.path.join(HERE, "golden", f"{name}_ema.safetensors"))
+    spec = F.infer_spec(sd, args)
+    assert (spec.kind, spec.state_dim, spec.context_dim, spec.horizon, tuple(spec.dim_mults)) == ("unet", 1, 4, 32, (1, 2, 4))
+    assert args["n_diffusion_steps"] == 25 and args["variance_schedule"] == "exponential"
+    net = nets.ConditionedTemporalUnet(state_dim=1, context_dim=4).eval()
+    net.load_state_dict({k[6:]: v for k, v in sd.items() if k.startswith("model.")}, strict=True)
+    assert sum(p.numel() for p in net.parameters()) == 1000033

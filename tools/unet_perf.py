@@ -2,7 +2,7 @@
 import sys, os, time, argparse
 import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec
+from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec, force_unet_path
 from oracle import nets
 ap = argparse.ArgumentParser()
 ap.add_argument("--B", type=int, default=16384)
@@ -15,9 +15,11 @@ ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--schedule", default="exponential")
 ap.add_argument("--dtype", default="f32x3", choices=["f32", "f32x3", "f16"])
 ap.add_argument("--fuse", default="", help="MPCD_UNET_FUSE (0 never, 1 always, empty: measured)")
+ap.add_argument("--path", default="auto", choices=["auto", "layered", "fused"], help="mpcd_unet_force_path")
 a = ap.parse_args()
 if a.fuse:
     os.environ["MPCD_UNET_FUSE"] = a.fuse
+force_unet_path(a.path)
 torch.manual_seed(0)
 net = nets.ConditionedTemporalUnet(state_dim=a.d, context_dim=a.C)
 plan = DiffusionMPC(NetSpec("unet", a.d, a.H, a.C, dtype=a.dtype), net.state_dict(), variance_schedule=a.schedule, n_diffusion_steps=a.N)
@@ -32,5 +34,5 @@ for _ in range(a.reps):
     evals = a.steps + 1
     mac = {32: 9122560, 64: 18209152}.get(a.H, 0) + 896 * (a.C - 5) + 224 * a.H * (a.d - 1)
     fl = a.B * evals * 2 * 2 * mac
-    print(f"{a.dtype} fuse={a.fuse or 'auto'} B={a.B} H={a.H}: {el*1e3:.1f} ms for {evals} CFG net evals -> {el/evals*1e3:.2f} ms/eval, "
+    print(f"{a.dtype} path={a.path} fuse={a.fuse or 'auto'} B={a.B} H={a.H}: {el*1e3:.1f} ms for {evals} CFG net evals -> {el/evals*1e3:.2f} ms/eval, "
           f"{fl/el/1e12:.1f} TFLOP/s, {a.B/el*evals/101:.0f} cand/s at 101 evals")
