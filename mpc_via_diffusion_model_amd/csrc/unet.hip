@@ -15,6 +15,8 @@
 // before one coalesced channels-last store. The denoise update is a separate elementwise kernel.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -868,12 +870,34 @@ int sample_fused(const mpcd_net_desc &d, const UnetWeights &W, const UnetSampleA
     hipLaunchKernelGGL(init_x_kernel, dim3(g1), dim3(threads), 0, st, xs, a.batch, flat, a.noise, a.seed,
                        a.global_offset, a.chain);
     f.x = xs;
+    // diagnostics: MPCD_FUSED_PROF=<file> writes the per-op s_memtime stamps of the third step's first workgroups
+    static const char *prof_path = getenv("MPCD_FUSED_PROF");
+    uint64_t *prof = nullptr;
+    const size_t prof_n = (size_t)unet_fused_prof_wgs() * unet_fused_n_ops(pl) * 4;
+    if (prof_path && a.n_steps > 2 && hipMalloc(&prof, prof_n * 8) == hipSuccess) (void)hipMemsetAsync(prof, 0, prof_n * 8, st);
     for (int s = 0; s < a.n_steps; ++s) {
         f.tp = a.tproj + (size_t)s * a.cond_total;
         f.step = s;
         f.last = s == a.n_steps - 1 ? 1 : 0;
+        f.prof = s == 2 ? prof : nullptr;
         hipError_t e = unet_fused_step(pl, f, st);
         if (e != hipSuccess) return uerr(MPCD_EHIP, std::string("fused U-Net: ") + hipGetErrorString(e));
+    }
+    if (prof) {
+        std::vector<uint64_t> h(prof_n);
+        if (hipStreamSynchronize(st) == hipSuccess && hipMemcpy(h.data(), prof, prof_n * 8, hipMemcpyDeviceToHost) == hipSuccess)
+            if (FILE *fp = fopen(prof_path, "wb")) {
+                const int32_t hdr[2] = {unet_fused_prof_wgs(), unet_fused_n_ops(pl)};
+                fwrite(hdr, 4, 2, fp);
+                fwrite(h.data(), 8, h.size(), fp);
+                for (int i = 0; i < unet_fused_n_ops(pl); ++i) {
+                    int32_t info[6];
+                    unet_fused_op_info(pl, i, info);
+                    fwrite(info, 4, 6, fp);
+                }
+                fclose(fp);
+            }
+        (void)hipFree(prof);
     }
     if (amq)
         hipLaunchKernelGGL(chain_absmax_kernel, dim3((unsigned)((a.batch + 255) / 256)), dim3(256), 0, st, amq, a.batch,

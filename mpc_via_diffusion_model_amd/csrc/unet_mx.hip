@@ -851,9 +851,10 @@ hipError_t prep_geom(int kind, ConvMK &k, std::string *why)
         k.halo_l = 0;
         k.halo_r = T - 1;
     }
-    // per-position stride: an odd number of 16-byte units
-    int cs = cinp * 2;
-    if (((cs / 16) & 1) == 0) cs += 16;
+    // per-position stride = 32 mod 64 bytes: each ds_read_b128 lane group of a B-fragment read (16 columns x
+    // 4 lane quarters, unet_fused.hip cs_of) covers the 64 banks once
+    int cs = (cinp * 2 + 15) / 16 * 16;
+    while (cs % 64 != 32) cs += 16;
     k.cs = cs;
     if ((k.in_h || k.res_h || k.out_h) &&
         (cinp != k.cinp || (k.in_h && ((k.ca & 7) || (k.cb & 7))) || (k.out_h && (k.cout & 3)))) {

@@ -119,7 +119,7 @@ def test_fused_philox_shards_and_layered_agree(dtype, H, d, C, fused):
 def test_fused_forced_on_uncovered_net_raises():
     net = make_unet(2, 3, mults=(1, 2, 4, 8), seed=1)
     plan = DiffusionMPC(NetSpec("unet", 2, 64, 3, dim_mults=(1, 2, 4, 8), dtype="f32x3"), net.state_dict(),
-                        n_diffusion_steps=10)
+                        variance_schedule="cosine", n_diffusion_steps=10)
     force_unet_path("fused")
     try:
         with pytest.raises(Exception, match="fused"):
