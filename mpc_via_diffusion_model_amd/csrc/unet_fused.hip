@@ -58,6 +58,7 @@ struct COp {
     int cinp, kc, nt_sh, cout, lin, lout;
     int half;              // NC = NCB / 2 column tiles per wave (else NCB = R * H / 64)
     int cpg_sh;            // log2 channels per GroupNorm group
+    int wpr;               // waves per row of the output (GroupNorm partial sums cross waves through LDS when > 1)
     int alias_in;          // the output overwrites the GEMM input region (barrier before the epilogue)
     int spill;             // also write the output to the skip scratch (RESTORE: read it back)
     CView in, res, out;
@@ -65,7 +66,7 @@ struct COp {
 constexpr int kMaxOps = 40;
 struct Prog {
     COp ops[kMaxOps];
-    int n, plb, e_off, stat_off, lds, part_floats, skip_elems_per_row, ok;
+    int n, plb, e_off, stat_off, lds, skip_elems_per_row, ok;
     CView xv;  // staged x: 8 channels, its own 2 + 5 zero positions per row
 };
 
@@ -107,10 +108,9 @@ constexpr Prog make_prog()
     regZ = (regZ + 15) / 16 * 16;
     const int offA = 0, offB = regA, offZ = 2 * regA;
     pg.plb = offZ + regZ;
-    pg.stat_off = P * pg.plb;
     pg.e_off = offZ;
-    pg.part_floats = R * (H >= 16 ? H / 16 : 1) * kGroups * 4;
-    pg.lds = pg.stat_off + 4 * (pg.part_floats + R * kGroups * 2);
+    pg.stat_off = P * pg.plb;
+    pg.lds = pg.stat_off + 2 * 4 * R * kGroups * 2;  // cross-wave GroupNorm partials [S1 | S2][row][group][2]
     auto view = [](int region, int L, int C, int ctot, int ch0) {
         CView v{};
         v.cs = cs_of(ctot ? ctot : C);
@@ -149,6 +149,10 @@ constexpr Prog make_prog()
         if (epi == FE_GN || epi == FE_GN_COND || epi == FE_GN_RES) {
             o.cpg_sh = ilog2c(cout / kGroups);
             if (o.cpg_sh < 2 || o.cpg_sh > 4 || o.lout < 8) pg.ok = 0;
+            // a wave's column tiles are whole rows (statistics in registers) or 1/2 of one row (partials
+            // exchanged through LDS)
+            o.wpr = o.lout > 16 && nc > 0 && (nc * 16) % o.lout ? o.lout / (nc * 16) : 1;
+            if (o.wpr > 2 || (o.wpr == 2 && o.lout != 2 * nc * 16)) pg.ok = 0;
         }
         o.in = in;
         o.out = out;
@@ -285,6 +289,34 @@ MPCD_DEV float rows_pair_sum(float v)
 MPCD_DEV float rows_quad_sum(float v)
 {
     return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x143, 0x8, 0xF, false));
+}
+
+// lane l + xor 16 / xor 32 partner sums on gfx950's permlane swaps (VALU, no LDS): with both operands the
+// same register, the two results of v_permlane{16,32}_swap hold (own, partner) in complementary lanes, so
+// their sum is v + v[l ^ 16] (v + v[l ^ 32]) in every lane
+MPCD_DEV float xor16_sum(float v)
+{
+    const unsigned u = __builtin_bit_cast(unsigned, v);
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    const unsigned own = r[0], other = r[1];  // (bit_cast straight off r[1] reads r[0]: clang, ROCm 7.2)
+    return __builtin_bit_cast(float, own) + __builtin_bit_cast(float, other);
+}
+MPCD_DEV float xor32_sum(float v)
+{
+    const unsigned u = __builtin_bit_cast(unsigned, v);
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    const unsigned own = r[0], other = r[1];  // (bit_cast straight off r[1] reads r[0]: clang, ROCm 7.2)
+    return __builtin_bit_cast(float, own) + __builtin_bit_cast(float, other);
+}
+// sum over a (row segment, GroupNorm group): SEG columns (8 or 16 lanes of one DPP row) x the group's lane
+// quarters (QMASK + 1 of them: 1, 2 or 4); every lane of the group gets the total
+template <int SEG, int QMASK>
+MPCD_DEV float group_sum(float v)
+{
+    v = seg_sum<SEG>(v);
+    if constexpr (QMASK >= 1) v = xor16_sum(v);
+    if constexpr (QMASK >= 3) v = xor32_sum(v);
+    return v;
 }
 
 constexpr int kProfWgs = 64;
@@ -483,95 +515,94 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
 #pragma unroll
     for (int cc = 0; cc < NC; ++cc) acc[cc] = acc[cc] + bias;
 
+    if constexpr (I + 1 < N_OPS) prefetch_op<P, R, H, I + 1>(a, wave, lane, pre);  // lands during the epilogue
     prof_mark(a, N_OPS, I, 1);
-    // ---- GroupNorm statistics from the accumulators
-    float *part = reinterpret_cast<float *>(sm + ProgOf<P, R, H>::v.stat_off);  // [segment][group][S1, S2, shift, -]
-    float *stat = part + ProgOf<P, R, H>::v.part_floats;                     // [row][group][mean, rstd]
-    constexpr int CPG_SH = GN ? op.cpg_sh : 2;
-    const int g = n0 >> CPG_SH;
-    if constexpr (GN) {
-        constexpr int L = op.lout, SEG = L < 16 ? L : 16, SEG_SH = L < 16 ? 3 : 4;
-        constexpr int QMASK = (1 << (CPG_SH - 2)) - 1;  // lane quarters per group - 1: 0, 1 or 3
-        const int src = (col & ~(SEG - 1)) | ((q & ~QMASK) << 4);
+    // ---- GroupNorm statistics, in registers: the program's tilings give every wave whole rows (make_prog
+    // checks it), so each (row, group) lives in one wave - its 16-lane DPP rows (columns) and 1, 2 or 4 lane
+    // quarters (the group's channels). Exact two-pass: mean, then the centred sum of squares; every lane of the
+    // group ends with both. Fixed order: the same bits for any batch, workgroup or tiling of the other ops.
+    float mean[NC], rstd[NC];
+    static_assert(!(GN && op.alias_in), "GroupNorm ops write a region their GEMM does not read");
+    if constexpr (GN && op.wpr == 2) {
+        // a row spans two waves (the wave's NC tiles are one half of it): per-wave partial sums through LDS,
+        // added in wave order (the same bits for any batch or workgroup); two barriers per op
+        constexpr int QMASK = (1 << (op.cpg_sh - 2)) - 1;
+        constexpr float inv_n = 1.0f / (float)(op.lout << op.cpg_sh);
+        float *st = reinterpret_cast<float *>(sm + ProgOf<P, R, H>::v.stat_off);  // [2][R][kGroups][2]
+        const int row = cr[0], g = n0 >> op.cpg_sh, half = (t0 / NC) & 1;
+        const int slot = (row * kGroups + g) * 2;
+        const bool leader = col == 0 && (q & QMASK) == 0;
+        float s1 = 0.f;
 #pragma unroll
-        for (int cc = 0; cc < NC; ++cc) {
-            // shift = the segment's first value of the group: the sums are of (x - shift) = O(std)
-            const float sh = __shfl(acc[cc][0], src);
-            float s1 = 0.f, s2 = 0.f;
+        for (int cc = 0; cc < NC; ++cc) s1 += (acc[cc][0] + acc[cc][1]) + (acc[cc][2] + acc[cc][3]);
+        s1 = group_sum<16, QMASK>(s1);
+        if (leader) st[slot + half] = s1;
+        lds_barrier();
+        const f32x2 p1 = *reinterpret_cast<const f32x2 *>(st + slot);
+        const float m = (p1.x + p1.y) * inv_n;
+        float s2 = 0.f;
+#pragma unroll
+        for (int cc = 0; cc < NC; ++cc)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const float dv = acc[cc][e] - sh;
-                s1 += dv;
+                const float dv = acc[cc][e] - m;
                 s2 += dv * dv;
             }
-            // the segment's columns (8 or 16 lanes of one DPP row), then the group's lane quarters (rows)
-            s1 = seg_sum<SEG>(s1);
-            s2 = seg_sum<SEG>(s2);
-            if constexpr (SEG == 16) {  // every lane of a row holds its row total: row_bcast chains (writer: last row)
-                if constexpr (QMASK >= 1) {
-                    s1 = rows_pair_sum(s1);
-                    s2 = rows_pair_sum(s2);
-                }
-                if constexpr (QMASK >= 3) {
-                    s1 = rows_quad_sum(s1);
-                    s2 = rows_quad_sum(s2);
-                }
-            } else {  // two 8-lane segments per row: symmetric exchanges across rows (every row gets the total)
-                if constexpr (QMASK >= 1) {
-                    s1 += __shfl_xor(s1, 16);
-                    s2 += __shfl_xor(s2, 16);
-                }
-                if constexpr (QMASK >= 3) {
-                    s1 += __shfl_xor(s1, 32);
-                    s2 += __shfl_xor(s2, 32);
+        s2 = group_sum<16, QMASK>(s2);
+        if (leader) st[2 * R * kGroups + slot + half] = s2;
+        lds_barrier();
+        const f32x2 p2 = *reinterpret_cast<const f32x2 *>(st + 2 * R * kGroups + slot);
+        const float rs = 1.0f / __fsqrt_rn((p2.x + p2.y) * inv_n + 1e-5f);
+#pragma unroll
+        for (int cc = 0; cc < NC; ++cc) {
+            mean[cc] = m;
+            rstd[cc] = rs;
+        }
+    } else if constexpr (GN) {
+        constexpr int L = op.lout, SEG = L < 16 ? L : 16, TPR = L > 16 ? L / 16 : 1;  // column tiles per row
+        constexpr int QMASK = (1 << (op.cpg_sh - 2)) - 1;  // lane quarters per group - 1: 0, 1 or 3
+        constexpr float inv_n = 1.0f / (float)(L << op.cpg_sh);
+        static_assert(NC % TPR == 0, "a wave's column tiles are whole rows");
+#pragma unroll
+        for (int j = 0; j < NC / TPR; ++j) {
+            float s1 = 0.f;
+#pragma unroll
+            for (int t = 0; t < TPR; ++t) {
+                const f32x4 &x = acc[j * TPR + t];
+                s1 += (x[0] + x[1]) + (x[2] + x[3]);
+            }
+            s1 = group_sum<SEG, QMASK>(s1);
+            const float m = s1 * inv_n;
+            float s2 = 0.f;
+#pragma unroll
+            for (int t = 0; t < TPR; ++t) {
+                const f32x4 &x = acc[j * TPR + t];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float dv = x[e] - m;
+                    s2 += dv * dv;
                 }
             }
-            if ((col & (SEG - 1)) == 0 && (q & QMASK) == QMASK) {
-                const int seg = ((t0 + cc) * 16 + col) >> SEG_SH;
-                *reinterpret_cast<f32x4 *>(part + (seg * kGroups + g) * 4) = f32x4{s1, s2, sh, 0.f};
+            s2 = group_sum<SEG, QMASK>(s2);
+            const float rs = 1.0f / __fsqrt_rn(s2 * inv_n + 1e-5f);
+#pragma unroll
+            for (int t = 0; t < TPR; ++t) {
+                mean[j * TPR + t] = m;
+                rstd[j * TPR + t] = rs;
             }
         }
-        lds_barrier();
-        if (tid < R * kGroups) {  // one (row, group) per thread: its equal-sized segments, fixed order
-            using acc_t = typename std::conditional<P == 1, float, double>::type;
-            constexpr int NSEG = L >> SEG_SH;  // 1, 2 or 4
-            constexpr acc_t n1 = (acc_t)(SEG << CPG_SH), inv_n1 = (acc_t)1 / n1;  // powers of two: exact
-            const int r = tid / kGroups, gg = tid - r * kGroups;
-            acc_t mk[NSEG], m2 = 0, msum = 0;
-#pragma unroll
-            for (int k = 0; k < NSEG; ++k) {
-                const f32x4 p = *reinterpret_cast<const f32x4 *>(part + ((r * NSEG + k) * kGroups + gg) * 4);
-                mk[k] = (acc_t)p[2] + (acc_t)p[0] * inv_n1;
-                m2 += (acc_t)p[1] - (acc_t)p[0] * (acc_t)p[0] * inv_n1;
-                msum += mk[k];
-            }
-            const acc_t mean = msum * ((acc_t)1 / (acc_t)NSEG);
-#pragma unroll
-            for (int k = 0; k < NSEG; ++k) m2 += n1 * (mk[k] - mean) * (mk[k] - mean);
-            const acc_t var = m2 * (inv_n1 * ((acc_t)1 / (acc_t)NSEG));
-            stat[2 * tid] = (float)mean;
-            stat[2 * tid + 1] = (float)((acc_t)1 / sqrt((var > 0 ? var : (acc_t)0) + (acc_t)1e-5));
-        }
-        lds_barrier();
     } else if constexpr (op.alias_in) {
         lds_barrier();
     }
-    if constexpr (I + 1 < N_OPS) prefetch_op<P, R, H, I + 1>(a, wave, lane, pre);  // lands during this epilogue
 
     prof_mark(a, N_OPS, I, 2);
     // ---- epilogue: GroupNorm affine -> Mish -> + cond / + residual, written as the next conv's planes.
     // LDS reads of every column tile first (statistics, residual), then the arithmetic, then the writes.
     f32x4 v[NC];
-    float mean[NC], rstd[NC];
     u32x2 rp[NC][P];
 #pragma unroll
     for (int cc = 0; cc < NC; ++cc) {
         v[cc] = acc[cc];
-        if constexpr (GN) {
-            const f32x2 ms = *reinterpret_cast<const f32x2 *>(stat + 2 * (cr[cc] * kGroups + g));
-            mean[cc] = ms.x;
-            rstd[cc] = ms.y;
-        }
         if constexpr (EPI == FE_GN_RES) {
             const char *s = sm + op.res.off + cr[cc] * op.res.rowB + co[cc] * op.res.cs + 2 * n0;
 #pragma unroll
@@ -758,13 +789,13 @@ struct Cfg {
     int P, R, H;
 };
 // the instantiated configurations (the LDS of R rows fits one CU: static_assert in the kernel)
-constexpr Cfg kCfgs[] = {{1, 6, 64}, {1, 4, 64}, {3, 4, 32}, {1, 8, 32}, {3, 2, 64}};
+constexpr Cfg kCfgs[] = {{1, 4, 64}, {3, 4, 32}, {1, 8, 32}, {3, 2, 64}};
 
 const Prog *prog_of(int P, int R, int H)
 {
 #define C_(p, r, h) \
     if (P == p && R == r && H == h) return &ProgOf<p, r, h>::v;
-    C_(1, 6, 64) C_(1, 4, 64) C_(3, 4, 32) C_(1, 8, 32) C_(3, 2, 64)
+    C_(1, 4, 64) C_(3, 4, 32) C_(1, 8, 32) C_(3, 2, 64)
 #undef C_
     return nullptr;
 }
@@ -783,7 +814,7 @@ hipError_t launch_any(int P, int R, int H, const FArgs &fa, unsigned grid, hipSt
 {
 #define C_(p, r, h) \
     if (P == p && R == r && H == h) return launch_cfg<p, r, h>(fa, grid, st);
-    C_(1, 6, 64) C_(1, 4, 64) C_(3, 4, 32) C_(1, 8, 32) C_(3, 2, 64)
+    C_(1, 4, 64) C_(3, 4, 32) C_(1, 8, 32) C_(3, 2, 64)
 #undef C_
     return hipErrorInvalidValue;
 }

@@ -38,23 +38,25 @@ def assert_traj_close(got, ref, rel=REL_TRAJ, abs_elem=ABS_ELEM, what=""):
 
 
 def oracle_sensitivity(run):
-    """Elementwise spread of the oracle itself when every Linear/Conv rounds from fp64 instead of fp32
-    (a 1-ulp-level perturbation). Unclamped DDIM is ill-conditioned (x0 = a*x - b*eps with a, b up to
+    """Elementwise spread of the oracle itself when every Linear/Conv/GroupNorm rounds from fp64 instead of
+    fp32 (a 1-ulp-level perturbation). Unclamped DDIM is ill-conditioned (x0 = a*x - b*eps with a, b up to
     2.6e6 at N=100), so its elementwise parity bar is this spread, not 1e-4; the trajectory bar stays."""
     import torch.nn as nn
     import torch.nn.functional as F
     ref = run()
-    saved = (nn.Linear.forward, nn.Conv1d.forward, nn.ConvTranspose1d.forward)
+    saved = (nn.Linear.forward, nn.Conv1d.forward, nn.ConvTranspose1d.forward, nn.GroupNorm.forward)
     nn.Linear.forward = lambda self, x: F.linear(x.double(), self.weight.double(), self.bias.double()).float()
     nn.Conv1d.forward = lambda self, x: F.conv1d(x.double(), self.weight.double(), self.bias.double(), self.stride,
                                                  self.padding).float()
     nn.ConvTranspose1d.forward = lambda self, x: F.conv_transpose1d(x.double(), self.weight.double(),
                                                                     self.bias.double(), self.stride,
                                                                     self.padding).float()
+    nn.GroupNorm.forward = lambda self, x: F.group_norm(x.double(), self.num_groups, self.weight.double(),
+                                                        self.bias.double(), self.eps).float()
     try:
         pert = run()
     finally:
-        nn.Linear.forward, nn.Conv1d.forward, nn.ConvTranspose1d.forward = saved
+        nn.Linear.forward, nn.Conv1d.forward, nn.ConvTranspose1d.forward, nn.GroupNorm.forward = saved
     r, p = ref.double(), pert.double()
     return ref, float(((p - r).abs() / r.abs().clamp_min(1.0)).max())
 

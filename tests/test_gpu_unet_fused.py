@@ -100,7 +100,8 @@ def test_fused_cfg_ddim_matches_oracle(fused):
 @pytest.mark.parametrize("dtype,H,d,C", [("f32x3", 32, 1, 2), ("f16", 64, 4, 12), ("f32x3", 64, 1, 5)])
 def test_fused_philox_shards_and_layered_agree(dtype, H, d, C, fused):
     """Philox mode: any split of the batch gives the same bits (the GroupNorm order does not depend on the
-    workgroup), and the layer-by-layer path agrees within the numerics' bar."""
+    workgroup), and the layer-by-layer path agrees within twice the numerics' bar (both sit within it of the
+    oracle)."""
     net = make_unet(d, C, seed=8)
     plan = _planner(net, d, H, C, N=25, dtype=dtype)
     ctx = torch.rand(1, C, generator=torch.Generator().manual_seed(3)) * 2 - 1
@@ -113,7 +114,8 @@ def test_fused_philox_shards_and_layered_agree(dtype, H, d, C, fused):
     lay = plan.sample_trajectories(ctx, B, H, seed=5)
     force_unet_path("fused")
     rel = float(((full - lay).flatten(1).norm(dim=1) / lay.flatten(1).norm(dim=1)).max())
-    assert rel <= (1e-4 if dtype == "f32x3" else 5e-2), rel
+    # each path is within the §8d bar (1e-4) of the oracle (tests above): they agree within twice that
+    assert rel <= (2e-4 if dtype == "f32x3" else 5e-2), rel
 
 
 def test_fused_forced_on_uncovered_net_raises():
