@@ -319,6 +319,28 @@ MPCD_DEV float group_sum(float v)
     return v;
 }
 
+// packed fp32 (v_pk_fma / v_pk_mul / v_pk_add: two lanes' worth per 4-cycle issue; the epilogue is VALU-bound)
+MPCD_DEV f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+MPCD_DEV f32x2 lo2(const f32x4 &v) { return f32x2{v[0], v[1]}; }
+MPCD_DEV f32x2 hi2(const f32x4 &v) { return f32x2{v[2], v[3]}; }
+constexpr float kLog2e = 1.44269504088896341f, kLn2 = 0.693147180559945309f;
+// Mish of a pair given in log2 units (z = y log2 e): y (1 - 2 / (n (n + 2) + 2)), n = e^y (common.h mish); four
+// transcendentals, four packed ops
+MPCD_DEV f32x2 mish2_log2(f32x2 z)
+{
+    const f32x2 n = {__builtin_amdgcn_exp2f(z[0]), __builtin_amdgcn_exp2f(z[1])};
+    const f32x2 den = fma2(n, n + 2.0f, f32x2{2.0f, 2.0f});
+    const f32x2 r = {__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
+    return z * fma2(r, f32x2{-2.0f * kLn2, -2.0f * kLn2}, f32x2{kLn2, kLn2});
+}
+
+// 1 / sqrt(x) for x >= 1e-5 (variance + eps): v_rsq_f32 and one Newton step (fp32-exact to ~1 ulp)
+MPCD_DEV float rsqrt_nr(float x)
+{
+    const float r = __builtin_amdgcn_rsqf(x);
+    return r * __builtin_fmaf(-0.5f * x * r, r, 1.5f);
+}
+
 constexpr int kProfWgs = 64;
 MPCD_DEV void prof_mark(const FArgs &a, int n_ops, int oi, int k)
 {
@@ -489,11 +511,20 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
 #pragma unroll
             for (int cc = 0; cc < NC; ++cc) acc[cc] = mma<P>(A[PA<P>(i)], B[cc][PB<P>(i)], acc[cc]);
     };
-    u32x4 A[DA][P];
+    // the A ring: its first chunks were issued before the previous op's epilogue (P = 1: the prefetch registers
+    // themselves; P = 3: a copy, which schedules the six-product K loop better)
+    u32x4 Acopy[P == 1 ? 1 : DA][P];
+    u32x4(&A)[DA][P] = *[&]() -> u32x4(*)[DA][P] {
+        if constexpr (P == 1) {
+            return &pre.A;
+        } else {
 #pragma unroll
-    for (int s = 0; s < DA; ++s)
+            for (int s = 0; s < DA; ++s)
 #pragma unroll
-        for (int pl = 0; pl < P; ++pl) A[s][pl] = pre.A[s][pl];  // issued before the previous op's epilogue
+                for (int pl = 0; pl < P; ++pl) Acopy[s][pl] = pre.A[s][pl];
+            return &Acopy;
+        }
+    }();
     u32x4 B[DB][NC][P];
 #pragma unroll
     for (int s = 0; s < DB; ++s) load_b(B[s], s);
@@ -532,27 +563,26 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
         const int row = cr[0], g = n0 >> op.cpg_sh, half = (t0 / NC) & 1;
         const int slot = (row * kGroups + g) * 2;
         const bool leader = col == 0 && (q & QMASK) == 0;
-        float s1 = 0.f;
+        f32x2 p1 = lo2(acc[0]) + hi2(acc[0]);
 #pragma unroll
-        for (int cc = 0; cc < NC; ++cc) s1 += (acc[cc][0] + acc[cc][1]) + (acc[cc][2] + acc[cc][3]);
-        s1 = group_sum<16, QMASK>(s1);
+        for (int cc = 1; cc < NC; ++cc) p1 += lo2(acc[cc]) + hi2(acc[cc]);
+        const float s1 = group_sum<16, QMASK>(p1[0] + p1[1]);
         if (leader) st[slot + half] = s1;
         lds_barrier();
-        const f32x2 p1 = *reinterpret_cast<const f32x2 *>(st + slot);
-        const float m = (p1.x + p1.y) * inv_n;
-        float s2 = 0.f;
+        const f32x2 w1 = *reinterpret_cast<const f32x2 *>(st + slot);
+        const float m = (w1.x + w1.y) * inv_n;
+        const f32x2 mm = {-m, -m};
+        f32x2 p2 = {0.f, 0.f};
 #pragma unroll
-        for (int cc = 0; cc < NC; ++cc)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float dv = acc[cc][e] - m;
-                s2 += dv * dv;
-            }
-        s2 = group_sum<16, QMASK>(s2);
+        for (int cc = 0; cc < NC; ++cc) {
+            const f32x2 d0 = lo2(acc[cc]) + mm, d1 = hi2(acc[cc]) + mm;
+            p2 = fma2(d1, d1, fma2(d0, d0, p2));
+        }
+        const float s2 = group_sum<16, QMASK>(p2[0] + p2[1]);
         if (leader) st[2 * R * kGroups + slot + half] = s2;
         lds_barrier();
-        const f32x2 p2 = *reinterpret_cast<const f32x2 *>(st + 2 * R * kGroups + slot);
-        const float rs = 1.0f / __fsqrt_rn((p2.x + p2.y) * inv_n + 1e-5f);
+        const f32x2 w2 = *reinterpret_cast<const f32x2 *>(st + 2 * R * kGroups + slot);
+        const float rs = rsqrt_nr((w2.x + w2.y) * inv_n + 1e-5f);
 #pragma unroll
         for (int cc = 0; cc < NC; ++cc) {
             mean[cc] = m;
@@ -565,26 +595,20 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
         static_assert(NC % TPR == 0, "a wave's column tiles are whole rows");
 #pragma unroll
         for (int j = 0; j < NC / TPR; ++j) {
-            float s1 = 0.f;
+            f32x2 p1 = lo2(acc[j * TPR]) + hi2(acc[j * TPR]);
 #pragma unroll
-            for (int t = 0; t < TPR; ++t) {
-                const f32x4 &x = acc[j * TPR + t];
-                s1 += (x[0] + x[1]) + (x[2] + x[3]);
-            }
-            s1 = group_sum<SEG, QMASK>(s1);
+            for (int t = 1; t < TPR; ++t) p1 += lo2(acc[j * TPR + t]) + hi2(acc[j * TPR + t]);
+            const float s1 = group_sum<SEG, QMASK>(p1[0] + p1[1]);
             const float m = s1 * inv_n;
-            float s2 = 0.f;
+            const f32x2 mm = {-m, -m};
+            f32x2 p2 = {0.f, 0.f};
 #pragma unroll
             for (int t = 0; t < TPR; ++t) {
-                const f32x4 &x = acc[j * TPR + t];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float dv = x[e] - m;
-                    s2 += dv * dv;
-                }
+                const f32x2 d0 = lo2(acc[j * TPR + t]) + mm, d1 = hi2(acc[j * TPR + t]) + mm;
+                p2 = fma2(d1, d1, fma2(d0, d0, p2));
             }
-            s2 = group_sum<SEG, QMASK>(s2);
-            const float rs = 1.0f / __fsqrt_rn(s2 * inv_n + 1e-5f);
+            const float s2 = group_sum<SEG, QMASK>(p2[0] + p2[1]);
+            const float rs = rsqrt_nr(s2 * inv_n + 1e-5f);
 #pragma unroll
             for (int t = 0; t < TPR; ++t) {
                 mean[j * TPR + t] = m;
@@ -609,15 +633,15 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
             for (int pl = 0; pl < P; ++pl) rp[cc][pl] = *reinterpret_cast<const u32x2 *>(s + pl * PLB);
         }
     }
+    // GroupNorm affine in log2 units: z = ((x - mean) rstd gamma + beta) log2 e
+    const f32x2 gl0 = lo2(gw) * kLog2e, gl1 = hi2(gw) * kLog2e, bl0 = lo2(gb) * kLog2e, bl1 = hi2(gb) * kLog2e;
 #pragma unroll
     for (int cc = 0; cc < NC; ++cc) {
         if constexpr (GN) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float scale = rstd[cc] * gw[e];
-                const float shift = -scale * mean[cc] + gb[e];
-                v[cc][e] = mish(v[cc][e] * scale + shift);
-            }
+            const f32x2 rr = {rstd[cc], rstd[cc]}, mr = {-mean[cc] * rstd[cc], -mean[cc] * rstd[cc]};
+            const f32x2 y0 = mish2_log2(fma2(fma2(lo2(v[cc]), rr, mr), gl0, bl0));
+            const f32x2 y1 = mish2_log2(fma2(fma2(hi2(v[cc]), rr, mr), gl1, bl1));
+            v[cc] = f32x4{y0[0], y0[1], y1[0], y1[1]};
         }
         if constexpr (EPI == FE_GN_COND) {
             const bool masked = cr[cc] >= R / 2;
