@@ -143,7 +143,8 @@ size_t unet_fused_scratch_bytes(const UnetFusedPlan &pl, int64_t batch);
 int unet_fused_rows_per_wg(const UnetFusedPlan &pl);
 int unet_fused_n_ops(const UnetFusedPlan &pl);
 int unet_fused_prof_wgs();
-void unet_fused_op_info(const UnetFusedPlan &pl, int i, int32_t out[6]);  // kind, epi, cinp, cout, lout, k-chunks
+// kind, epi, cinp, cout, lout, k-chunks, n-tiles per wave, column tiles per wave
+void unet_fused_op_info(const UnetFusedPlan &pl, int i, int32_t out[8]);
 hipError_t unet_fused_step(const UnetFusedPlan &pl, const UnetFusedStep &s, hipStream_t st);
 // mpcd_unet_force_path: 0 = automatic, 1 = layer by layer, 2 = fused (error where it does not apply)
 void unet_force_path(int path);

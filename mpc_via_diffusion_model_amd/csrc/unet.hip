@@ -506,7 +506,10 @@ int unet_prepare(const mpcd_net_desc &d, size_t, const TensorLookup &dev, const 
     W.ready = true;
     W.fused.reset();
     W.fused_why.clear();
-    if (UnetFusedPlan *fp = unet_fused_prepare(d, W, 0, &W.fused_why)) W.fused.reset(fp, unet_fused_free);
+    // MPCD_FUSED_ROWS=<R>: the fused program with R rows per workgroup (tuning experiments; default: the first
+    // instantiated configuration of the net's numerics and horizon)
+    static const int fused_rows = getenv("MPCD_FUSED_ROWS") ? atoi(getenv("MPCD_FUSED_ROWS")) : 0;
+    if (UnetFusedPlan *fp = unet_fused_prepare(d, W, fused_rows, &W.fused_why)) W.fused.reset(fp, unet_fused_free);
     return MPCD_OK;
 }
 
@@ -891,9 +894,9 @@ int sample_fused(const mpcd_net_desc &d, const UnetWeights &W, const UnetSampleA
                 fwrite(hdr, 4, 2, fp);
                 fwrite(h.data(), 8, h.size(), fp);
                 for (int i = 0; i < unet_fused_n_ops(pl); ++i) {
-                    int32_t info[6];
+                    int32_t info[8];
                     unet_fused_op_info(pl, i, info);
-                    fwrite(info, 4, 6, fp);
+                    fwrite(info, 4, 8, fp);
                 }
                 fclose(fp);
             }

@@ -18,11 +18,13 @@
 // The network is fixed, so the program (the 36 ops: convs + the h1 restore, their LDS views and tilings) is
 // a compile-time table per (numerics P, rows R, horizon H): every shape, offset and branch of the device
 // code is a constant; only the weight pointers come from a small runtime table (FPtr). Per conv: implicit
-// GEMM on v_mfma_f32_16x16x32_{f16,bf16} - wave w owns n-tile (w mod NT) and NC consecutive 16-column tiles
-// of the R x L output columns (NC = R*H/64 or half that; every wave has the same work); GroupNorm
-// statistics straight from the accumulators (shifted sums per 16-column segment, DPP reductions, segments
-// combined in a fixed order: deterministic, independent of the batch and of the workgroup); the epilogue
-// (bias, GroupNorm affine -> Mish -> + cond / + residual) in registers, written as the next conv's planes.
+// GEMM on v_mfma_f32_16x16x32_{f16,bf16} - wave w owns NTW (1 or 2) consecutive n-tiles and NCW consecutive
+// 16-column tiles of the R x L output columns (every wave has the same work; two n-tiles per wave read every
+// B fragment once for two MFMAs: the LDS read rate is otherwise the MFMA rate); GroupNorm statistics straight
+// from the accumulators (exact two-pass, DPP / permlane reductions inside the wave, or per-wave partials
+// through LDS when a row spans two waves; fixed order: deterministic, independent of the batch and of the
+// workgroup); the epilogue (bias, GroupNorm affine -> Mish -> + cond / + residual) in packed-fp32 registers,
+// written as the next conv's planes.
 #include <hip/hip_runtime.h>
 
 #include <string.h>
@@ -56,7 +58,7 @@ struct CView {
 struct COp {
     int kind, epi, layer;  // layer: index in UnetWeights::layers (the RESTORE op: the spilling conv's)
     int cinp, kc, nt_sh, cout, lin, lout;
-    int half;              // NC = NCB / 2 column tiles per wave (else NCB = R * H / 64)
+    int ntw_sh, ncw;       // log2 n-tiles per wave; 16-column tiles per wave
     int cpg_sh;            // log2 channels per GroupNorm group
     int wpr;               // waves per row of the output (GroupNorm partial sums cross waves through LDS when > 1)
     int alias_in;          // the output overwrites the GEMM input region (barrier before the epilogue)
@@ -88,12 +90,12 @@ constexpr int ilog2c(int v)
     return (1 << s) == v ? s : -1;
 }
 
-template <int P, int R, int H>
+template <int P, int R, int H, int NTW_MAX>
 constexpr Prog make_prog()
 {
     Prog pg{};
     pg.ok = 1;
-    const int H1 = H / 2, H2 = H / 4, NCB = R * H / 64;
+    const int H1 = H / 2, H2 = H / 4;
     // per-plane regions: A and B hold any level tensor, Z the third tensor of a projection block, the
     // concatenated up-path inputs, the staged x and the fp32 eps. Activation views share their zero halos
     // between rows (row r's positions L, L+1 are row r+1's -2, -1: R * (L + 2) + 2 positions per view).
@@ -140,20 +142,24 @@ constexpr Prog make_prog()
         o.cout = cout;
         o.lin = lin;
         o.lout = kind == FK_DOWN3 ? lin / 2 : kind == FK_UP4 ? 2 * lin : lin;
-        const int wc = nt >= 1 && nt <= 8 ? 8 / nt : 1;
-        const int ct = kind == FK_UP4 ? 2 * (R * lin / 16) : R * o.lout / 16;
-        const int nc = ct % wc == 0 ? ct / wc : -1;
-        o.half = nc == NCB / 2 ? 1 : 0;
-        if ((nc != NCB && nc != NCB / 2) || o.nt_sh < 0) pg.ok = 0;
-        if (kind == FK_UP4 && nc > 0 && (R * lin / 16) % nc) pg.ok = 0;  // a wave's tiles in one parity
-        if (epi == FE_GN || epi == FE_GN_COND || epi == FE_GN_RES) {
-            o.cpg_sh = ilog2c(cout / kGroups);
-            if (o.cpg_sh < 2 || o.cpg_sh > 4 || o.lout < 8) pg.ok = 0;
-            // a wave's column tiles are whole rows (statistics in registers) or 1/2 of one row (partials
-            // exchanged through LDS)
-            o.wpr = o.lout > 16 && nc > 0 && (nc * 16) % o.lout ? o.lout / (nc * 16) : 1;
-            if (o.wpr > 2 || (o.wpr == 2 && o.lout != 2 * nc * 16)) pg.ok = 0;
+        const int ct = kind == FK_UP4 ? 2 * (R * lin / 16) : R * o.lout / 16;  // column tiles
+        const bool gn = epi == FE_GN || epi == FE_GN_COND || epi == FE_GN_RES;
+        o.cpg_sh = gn ? ilog2c(cout / kGroups) : 0;
+        if (gn && (o.cpg_sh < 2 || o.cpg_sh > 4 || o.lout < 8)) pg.ok = 0;
+        // tiling: two n-tiles per wave where the op has them and the columns split evenly, else one; a wave's
+        // columns in one UP4 parity, and (GroupNorm) whole rows or one half of a row
+        o.ntw_sh = -1;
+        for (int w = (nt >= 2 && NTW_MAX >= 2) ? 1 : 0; w >= 0 && o.ntw_sh < 0; --w) {
+            const int ntg = nt >> w, wc = ntg >= 1 && ntg <= 8 ? 8 / ntg : 0;
+            const int ncw = wc && ct % wc == 0 ? ct / wc : 0;
+            if (ncw < 1 || (ncw << w) > 4 || (kind == FK_UP4 && (R * lin / 16) % ncw)) continue;
+            const int wpr = gn && o.lout > 16 && (ncw * 16) % o.lout ? o.lout / (ncw * 16) : 1;
+            if (wpr > 2 || (wpr == 2 && o.lout != 2 * ncw * 16)) continue;
+            o.ntw_sh = w;
+            o.ncw = ncw;
+            o.wpr = wpr;
         }
+        if (o.ntw_sh < 0 || o.nt_sh < 0) pg.ok = 0;
         o.in = in;
         o.out = out;
         if (res) o.res = *res;
@@ -231,7 +237,7 @@ constexpr Prog make_prog()
 
 template <int P, int R, int H>
 struct ProgOf {
-    static constexpr Prog v = make_prog<P, R, H>();
+    static constexpr Prog v = make_prog<P, R, H, 1>();
 };
 
 // ---- runtime tables and kernel arguments
@@ -350,14 +356,16 @@ MPCD_DEV void prof_mark(const FArgs &a, int n_ops, int oi, int k)
 
 template <int P> constexpr int kDA = P == 1 ? 4 : 2;  // A (weight) chunks in flight: L2 latency
 constexpr int kDB = 2;                                  // B (LDS) chunks in flight
+constexpr int kNTW = 2;                                 // n-tiles per wave, at most
 template <int P> struct APre {                          // the next conv's first A chunks, loaded ahead
-    u32x4 A[kDA<P>][P];
+    u32x4 A[kDA<P>][kNTW][P];
 };
 
 template <int P, int R, int H, int I>
 struct OpGeo {  // the wave-independent constants of op I
     static constexpr COp op = ProgOf<P, R, H>::v.ops[I];
-    static constexpr int NCB = R * H / 64, NC = op.half ? NCB / 2 : NCB, NT = 1 << op.nt_sh;
+    static constexpr int NT = 1 << op.nt_sh, NTW = 1 << op.ntw_sh, NCW = op.ncw;
+    static constexpr int ntg_sh = op.nt_sh - op.ntw_sh;                // log2 n-tile groups
     static constexpr int lcol = op.kind == FK_UP4 ? op.lin : op.lout;  // columns per row and parity
     static constexpr int lsh = ilog2c(lcol);
     static constexpr int tiles_par = R * op.lin / 16;                  // UP4: column tiles per parity
@@ -370,24 +378,27 @@ MPCD_DEV __amdgpu_buffer_rsrc_t weight_rsrc(const uint16_t *w, int bytes)
 {
     return __builtin_amdgcn_make_buffer_rsrc((void *)w, (short)0, bytes, 0x00020000);
 }
-template <int P, int NT, int KC>
-MPCD_DEV void load_a(const __amdgpu_buffer_rsrc_t &rs, int par, int nt, int kc, int lane, u32x4 (&A)[P])
+// k-chunk kc of n-tiles nt0 .. nt0 + NTW - 1 (every plane): one 16-byte buffer load per lane each
+template <int P, int NT, int KC, int NTW>
+MPCD_DEV void load_a(const __amdgpu_buffer_rsrc_t &rs, int par, int nt0, int kc, int lane, u32x4 (&A)[kNTW][P])
 {
 #pragma unroll
-    for (int pl = 0; pl < P; ++pl) {
-        const int soff = __builtin_amdgcn_readfirstlane(((((par * NT + nt) * KC) + kc) * P + pl) * 1024);
-        A[pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, soff, 0));
-    }
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int pl = 0; pl < P; ++pl) {
+            const int soff = __builtin_amdgcn_readfirstlane(((((par * NT + nt0 + j) * KC) + kc) * P + pl) * 1024);
+            A[j][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, soff, 0));
+        }
 }
 
-// this wave's n-tile, first column tile and parity (UP4) in op I
+// this wave's first n-tile, first column tile and parity (UP4) in op I
 template <int P, int R, int H, int I>
-MPCD_DEV void wave_tiles(int wave, int &nt, int &t0, int &par)
+MPCD_DEV void wave_tiles(int wave, int &nt0, int &t0, int &par)
 {
     using G = OpGeo<P, R, H, I>;
-    nt = wave & (G::NT - 1);
-    t0 = (wave >> G::op.nt_sh) * G::NC;
-    par = G::op.kind == FK_UP4 && t0 >= G::tiles_par ? 1 : 0;  // host: NC divides tiles_par
+    nt0 = (wave & ((1 << G::ntg_sh) - 1)) << G::op.ntw_sh;
+    t0 = (wave >> G::ntg_sh) * G::NCW;
+    par = G::op.kind == FK_UP4 && t0 >= G::tiles_par ? 1 : 0;  // make_prog: NCW divides tiles_par
 }
 
 // issue the first A chunks of op I for this wave (so they land while the previous op's epilogue runs)
@@ -397,11 +408,12 @@ MPCD_DEV void prefetch_op(const FArgs &a, int wave, int lane, APre<P> &pre)
     using G = OpGeo<P, R, H, I>;
     if constexpr (G::op.kind != FK_RESTORE) {
         CPtr &pp = reinterpret_cast<CPtr *>((uintptr_t)a.ptrs)[I];
-        int nt, t0, par;
-        wave_tiles<P, R, H, I>(wave, nt, t0, par);
+        int nt0, t0, par;
+        wave_tiles<P, R, H, I>(wave, nt0, t0, par);
         const __amdgpu_buffer_rsrc_t rs = weight_rsrc<P>(pp.w, G::wbytes);
 #pragma unroll
-        for (int s = 0; s < kDA<P>; ++s) load_a<P, G::NT, G::op.kc>(rs, par, nt, s < G::op.kc ? s : G::op.kc - 1, lane, pre.A[s]);
+        for (int s = 0; s < kDA<P>; ++s)
+            load_a<P, G::NT, G::op.kc, G::NTW>(rs, par, nt0, s < G::op.kc ? s : G::op.kc - 1, lane, pre.A[s]);
     }
 }
 
@@ -426,44 +438,52 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
     extern __shared__ __attribute__((aligned(16))) char sm[];
     using G = OpGeo<P, R, H, I>;
     constexpr COp op = G::op;
-    constexpr int NC = G::NC, NT = G::NT, KC = op.kc, KIND = op.kind, EPI = op.epi;
+    constexpr int NCW = G::NCW, NTW = G::NTW, NT = G::NT, KC = op.kc, KIND = op.kind, EPI = op.epi;
     constexpr int DA = kDA<P>, DB = kDB;
     constexpr int PLB = ProgOf<P, R, H>::v.plb, N_OPS = ProgOf<P, R, H>::v.n;
     constexpr bool GN = EPI == FE_GN || EPI == FE_GN_COND || EPI == FE_GN_RES;
+    static_assert(!(GN && op.alias_in), "GroupNorm ops write a region their GEMM does not read");
+    static_assert(EPI != FE_EPS || NTW == 1, "the eps conv has one n-tile");
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int col = lane & 15, q = lane >> 4;
-    int nt, t0, par;
-    wave_tiles<P, R, H, I>(wave, nt, t0, par);
-    const int n0 = nt * 16 + 4 * q;
+    int nt0, t0, par;
+    wave_tiles<P, R, H, I>(wave, nt0, t0, par);
+    int n0[NTW];  // first of the lane's 4 output channels, per n-tile of the wave
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) n0[j] = (nt0 + j) * 16 + 4 * q;
     CPtr &pp = reinterpret_cast<CPtr *>((uintptr_t)a.ptrs)[I];
 
     // ---- this op's per-channel parameters, loaded now so they land during the GEMM (the parameter blob is only
     // 4-byte aligned: scalar loads for bias / GroupNorm affine)
-    f32x4 bias = {0.f, 0.f, 0.f, 0.f}, gw = bias, gb = bias, cv0 = bias, cv1 = bias;
-    if constexpr (EPI == FE_EPS) {
+    // cond: cv1 = the masked branch's Linear(Mish(cat(t_emb, 0))) (the time part), cvs = the shared context
+    // part (when the context is one row) - both loaded unconditionally (no branch, no wait before the GEMM)
+    const bool shared_cp = a.cp && !a.cp_stride;
+    f32x4 bias[NTW], gw[NTW], gb[NTW], cvs[NTW], cv1[NTW];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) bias[e] = n0 + e < a.d ? pp.bias[n0 + e] : 0.f;
-    } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bias[e] = pp.bias[n0 + e];
-    }
-    if constexpr (GN) {
+    for (int j = 0; j < NTW; ++j) {
+        bias[j] = gw[j] = gb[j] = cvs[j] = cv1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            gw[e] = pp.gnw[n0 + e];
-            gb[e] = pp.gnb[n0 + e];
+            if constexpr (EPI == FE_EPS)
+                bias[j][e] = n0[j] + e < a.d ? pp.bias[n0[j] + e] : 0.f;
+            else
+                bias[j][e] = pp.bias[n0[j] + e];
+            if constexpr (GN) {
+                gw[j][e] = pp.gnw[n0[j] + e];
+                gb[j][e] = pp.gnb[n0[j] + e];
+            }
         }
-    }
-    if constexpr (EPI == FE_GN_COND) {
-        cv1 = ldg4(a.tp + pp.cond_off + n0);  // masked branch: Linear(Mish(cat(t_emb, 0))) = the time part
-        cv0 = (a.cp && !a.cp_stride) ? cv1 + ldg4(a.cp + pp.cond_off + n0) : cv1;
+        if constexpr (EPI == FE_GN_COND) {
+            cv1[j] = ldg4(a.tp + pp.cond_off + n0[j]);
+            cvs[j] = ldg4((shared_cp ? a.cp : a.tp) + pp.cond_off + n0[j]);
+        }
     }
 
     // ---- columns of the wave's tiles: (row, output position) and the tap-0 input position
-    int bb[NC], cr[NC], co[NC];
+    int bb[NCW], cr[NCW], co[NCW];
 #pragma unroll
-    for (int cc = 0; cc < NC; ++cc) {
+    for (int cc = 0; cc < NCW; ++cc) {
         int c = (t0 + cc) * 16 + col, pos0;
         if constexpr (KIND == FK_UP4) {
             c -= par * G::tiles_par * 16;
@@ -479,10 +499,12 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
         bb[cc] = op.in.off + cr[cc] * op.in.rowB + pos0 * op.in.cs;
     }
 
-    // ---- implicit GEMM: acc[cc] = channels nt*16 + 4q + e of column tile t0 + cc (bias added after)
-    f32x4 acc[NC];
+    // ---- implicit GEMM: acc[j][cc] = channels (nt0 + j)*16 + 4q + e of column tile t0 + cc (bias added after)
+    f32x4 acc[NTW][NCW];
 #pragma unroll
-    for (int cc = 0; cc < NC; ++cc) acc[cc] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int cc = 0; cc < NCW; ++cc) acc[j][cc] = f32x4{0.f, 0.f, 0.f, 0.f};
     const __amdgpu_buffer_rsrc_t rs = weight_rsrc<P>(pp.w, G::wbytes);
     // K walk: cinp >= 32: chunk kc = tap kc >> log2(cinp/32), channels (kc mod (cinp/32)) * 32 + 8q; cinp = 8:
     // one chunk = 4 taps, lane quarter q takes tap 4kc + q, channels 0..7
@@ -498,34 +520,38 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
         }
         return (KIND == FK_UP4 ? -tap : tap) * op.in.cs + 2 * ci;
     };
-    auto load_b = [&](u32x4 (&B)[NC][P], int kc) {
+    auto load_b = [&](u32x4 (&B)[NCW][P], int kc) {
         const int ko = koff(kc < KC ? kc : KC - 1);
 #pragma unroll
-        for (int cc = 0; cc < NC; ++cc)
+        for (int cc = 0; cc < NCW; ++cc)
 #pragma unroll
             for (int pl = 0; pl < P; ++pl) B[cc][pl] = *reinterpret_cast<const u32x4 *>(sm + bb[cc] + ko + pl * PLB);
     };
-    auto mmas = [&](const u32x4 (&A)[P], const u32x4 (&B)[NC][P]) {
+    auto mmas = [&](const u32x4 (&A)[kNTW][P], const u32x4 (&B)[NCW][P]) {
 #pragma unroll
         for (int i = 0; i < NPROD(P); ++i)
 #pragma unroll
-            for (int cc = 0; cc < NC; ++cc) acc[cc] = mma<P>(A[PA<P>(i)], B[cc][PB<P>(i)], acc[cc]);
+            for (int j = 0; j < NTW; ++j)
+#pragma unroll
+                for (int cc = 0; cc < NCW; ++cc) acc[j][cc] = mma<P>(A[j][PA<P>(i)], B[cc][PB<P>(i)], acc[j][cc]);
     };
     // the A ring: its first chunks were issued before the previous op's epilogue (P = 1: the prefetch registers
     // themselves; P = 3: a copy, which schedules the six-product K loop better)
-    u32x4 Acopy[P == 1 ? 1 : DA][P];
-    u32x4(&A)[DA][P] = *[&]() -> u32x4(*)[DA][P] {
+    u32x4 Acopy[P == 1 ? 1 : DA][kNTW][P];
+    u32x4(&A)[DA][kNTW][P] = *[&]() -> u32x4(*)[DA][kNTW][P] {
         if constexpr (P == 1) {
             return &pre.A;
         } else {
 #pragma unroll
             for (int s = 0; s < DA; ++s)
 #pragma unroll
-                for (int pl = 0; pl < P; ++pl) Acopy[s][pl] = pre.A[s][pl];
+                for (int j = 0; j < NTW; ++j)
+#pragma unroll
+                    for (int pl = 0; pl < P; ++pl) Acopy[s][j][pl] = pre.A[s][j][pl];
             return &Acopy;
         }
     }();
-    u32x4 B[DB][NC][P];
+    u32x4 B[DB][NCW][P];
 #pragma unroll
     for (int s = 0; s < DB; ++s) load_b(B[s], s);
     constexpr int U = DA > DB ? DA : DB;  // DA and DB are powers of two: ring slots are compile-time
@@ -533,7 +559,10 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
         mmas(A[s % DA], B[s % DB]);
         load_b(B[s % DB], k + DB);
         const int kn = k + DA < KC ? k + DA : KC - 1;
-        load_a<P, NT, KC>(rs, par, nt, kn, lane, A[s % DA]);
+        load_a<P, NT, KC, NTW>(rs, par, nt0, kn, lane, A[s % DA]);
+        // keep the refills where they are: the scheduler would otherwise sink each load next to its use (to
+        // shorten live ranges), leaving one chunk in flight and the L2 latency exposed at every MFMA
+        __builtin_amdgcn_sched_barrier(0);
     };
     int kc = 0;
     for (; kc + U <= KC; kc += U) {
@@ -544,141 +573,160 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
     for (int s = 0; s < U - 1; ++s)
         if (kc + s < KC) step(kc + s, s);
 #pragma unroll
-    for (int cc = 0; cc < NC; ++cc) acc[cc] = acc[cc] + bias;
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int cc = 0; cc < NCW; ++cc) acc[j][cc] = acc[j][cc] + bias[j];
 
     if constexpr (I + 1 < N_OPS) prefetch_op<P, R, H, I + 1>(a, wave, lane, pre);  // lands during the epilogue
     prof_mark(a, N_OPS, I, 1);
-    // ---- GroupNorm statistics, in registers: the program's tilings give every wave whole rows (make_prog
-    // checks it), so each (row, group) lives in one wave - its 16-lane DPP rows (columns) and 1, 2 or 4 lane
-    // quarters (the group's channels). Exact two-pass: mean, then the centred sum of squares; every lane of the
-    // group ends with both. Fixed order: the same bits for any batch, workgroup or tiling of the other ops.
-    float mean[NC], rstd[NC];
-    static_assert(!(GN && op.alias_in), "GroupNorm ops write a region their GEMM does not read");
+    // ---- GroupNorm statistics per (row, group): a group's channels are 1, 2 or 4 lane quarters of one n-tile,
+    // its columns the DPP-row lanes of the wave's tiles in that row. Exact two-pass (mean, then the centred sum of
+    // squares); fixed order: the same bits for any batch, workgroup or tiling of the other ops.
+    float mean[NTW][NCW], rstd[NTW][NCW];
+    constexpr int QMASK = GN ? (1 << (op.cpg_sh - 2)) - 1 : 0;  // lane quarters per group - 1: 0, 1 or 3
     if constexpr (GN && op.wpr == 2) {
-        // a row spans two waves (the wave's NC tiles are one half of it): per-wave partial sums through LDS,
-        // added in wave order (the same bits for any batch or workgroup); two barriers per op
-        constexpr int QMASK = (1 << (op.cpg_sh - 2)) - 1;
+        // a row spans two waves (the wave's NCW tiles are one half of it): per-wave partial sums through LDS,
+        // added in wave order; two barriers per op
         constexpr float inv_n = 1.0f / (float)(op.lout << op.cpg_sh);
-        float *st = reinterpret_cast<float *>(sm + ProgOf<P, R, H>::v.stat_off);  // [2][R][kGroups][2]
-        const int row = cr[0], g = n0 >> op.cpg_sh, half = (t0 / NC) & 1;
-        const int slot = (row * kGroups + g) * 2;
+        float *st = reinterpret_cast<float *>(sm + ProgOf<P, R, H>::v.stat_off);  // [S1 | S2][row][group][half]
+        const int row = cr[0], half = (t0 / NCW) & 1;
         const bool leader = col == 0 && (q & QMASK) == 0;
-        f32x2 p1 = lo2(acc[0]) + hi2(acc[0]);
+        int slot[NTW];
+        float m[NTW];
 #pragma unroll
-        for (int cc = 1; cc < NC; ++cc) p1 += lo2(acc[cc]) + hi2(acc[cc]);
-        const float s1 = group_sum<16, QMASK>(p1[0] + p1[1]);
-        if (leader) st[slot + half] = s1;
-        lds_barrier();
-        const f32x2 w1 = *reinterpret_cast<const f32x2 *>(st + slot);
-        const float m = (w1.x + w1.y) * inv_n;
-        const f32x2 mm = {-m, -m};
-        f32x2 p2 = {0.f, 0.f};
+        for (int j = 0; j < NTW; ++j) {
+            slot[j] = (row * kGroups + (n0[j] >> op.cpg_sh)) * 2;
+            f32x2 p1 = lo2(acc[j][0]) + hi2(acc[j][0]);
 #pragma unroll
-        for (int cc = 0; cc < NC; ++cc) {
-            const f32x2 d0 = lo2(acc[cc]) + mm, d1 = hi2(acc[cc]) + mm;
-            p2 = fma2(d1, d1, fma2(d0, d0, p2));
+            for (int cc = 1; cc < NCW; ++cc) p1 += lo2(acc[j][cc]) + hi2(acc[j][cc]);
+            const float s1 = group_sum<16, QMASK>(p1[0] + p1[1]);
+            if (leader) st[slot[j] + half] = s1;
         }
-        const float s2 = group_sum<16, QMASK>(p2[0] + p2[1]);
-        if (leader) st[2 * R * kGroups + slot + half] = s2;
         lds_barrier();
-        const f32x2 w2 = *reinterpret_cast<const f32x2 *>(st + 2 * R * kGroups + slot);
-        const float rs = rsqrt_nr((w2.x + w2.y) * inv_n + 1e-5f);
 #pragma unroll
-        for (int cc = 0; cc < NC; ++cc) {
-            mean[cc] = m;
-            rstd[cc] = rs;
-        }
-    } else if constexpr (GN) {
-        constexpr int L = op.lout, SEG = L < 16 ? L : 16, TPR = L > 16 ? L / 16 : 1;  // column tiles per row
-        constexpr int QMASK = (1 << (op.cpg_sh - 2)) - 1;  // lane quarters per group - 1: 0, 1 or 3
-        constexpr float inv_n = 1.0f / (float)(L << op.cpg_sh);
-        static_assert(NC % TPR == 0, "a wave's column tiles are whole rows");
-#pragma unroll
-        for (int j = 0; j < NC / TPR; ++j) {
-            f32x2 p1 = lo2(acc[j * TPR]) + hi2(acc[j * TPR]);
-#pragma unroll
-            for (int t = 1; t < TPR; ++t) p1 += lo2(acc[j * TPR + t]) + hi2(acc[j * TPR + t]);
-            const float s1 = group_sum<SEG, QMASK>(p1[0] + p1[1]);
-            const float m = s1 * inv_n;
-            const f32x2 mm = {-m, -m};
+        for (int j = 0; j < NTW; ++j) {
+            const f32x2 w1 = *reinterpret_cast<const f32x2 *>(st + slot[j]);
+            m[j] = (w1.x + w1.y) * inv_n;
+            const f32x2 mm = {-m[j], -m[j]};
             f32x2 p2 = {0.f, 0.f};
 #pragma unroll
-            for (int t = 0; t < TPR; ++t) {
-                const f32x2 d0 = lo2(acc[j * TPR + t]) + mm, d1 = hi2(acc[j * TPR + t]) + mm;
+            for (int cc = 0; cc < NCW; ++cc) {
+                const f32x2 d0 = lo2(acc[j][cc]) + mm, d1 = hi2(acc[j][cc]) + mm;
                 p2 = fma2(d1, d1, fma2(d0, d0, p2));
             }
-            const float s2 = group_sum<SEG, QMASK>(p2[0] + p2[1]);
-            const float rs = rsqrt_nr(s2 * inv_n + 1e-5f);
+            const float s2 = group_sum<16, QMASK>(p2[0] + p2[1]);
+            if (leader) st[2 * R * kGroups + slot[j] + half] = s2;
+        }
+        lds_barrier();
 #pragma unroll
-            for (int t = 0; t < TPR; ++t) {
-                mean[j * TPR + t] = m;
-                rstd[j * TPR + t] = rs;
+        for (int j = 0; j < NTW; ++j) {
+            const f32x2 w2 = *reinterpret_cast<const f32x2 *>(st + 2 * R * kGroups + slot[j]);
+            const float rs = rsqrt_nr((w2.x + w2.y) * inv_n + 1e-5f);
+#pragma unroll
+            for (int cc = 0; cc < NCW; ++cc) {
+                mean[j][cc] = m[j];
+                rstd[j][cc] = rs;
             }
         }
+    } else if constexpr (GN) {  // every (row, group) inside the wave
+        constexpr int L = op.lout, SEG = L < 16 ? L : 16, TPR = L > 16 ? L / 16 : 1;  // column tiles per row
+        constexpr float inv_n = 1.0f / (float)(L << op.cpg_sh);
+        static_assert(NCW % TPR == 0, "a wave's column tiles are whole rows");
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < NCW / TPR; ++r) {
+                f32x2 p1 = lo2(acc[j][r * TPR]) + hi2(acc[j][r * TPR]);
+#pragma unroll
+                for (int t = 1; t < TPR; ++t) p1 += lo2(acc[j][r * TPR + t]) + hi2(acc[j][r * TPR + t]);
+                const float m = group_sum<SEG, QMASK>(p1[0] + p1[1]) * inv_n;
+                const f32x2 mm = {-m, -m};
+                f32x2 p2 = {0.f, 0.f};
+#pragma unroll
+                for (int t = 0; t < TPR; ++t) {
+                    const f32x2 d0 = lo2(acc[j][r * TPR + t]) + mm, d1 = hi2(acc[j][r * TPR + t]) + mm;
+                    p2 = fma2(d1, d1, fma2(d0, d0, p2));
+                }
+                const float rs = rsqrt_nr(group_sum<SEG, QMASK>(p2[0] + p2[1]) * inv_n + 1e-5f);
+#pragma unroll
+                for (int t = 0; t < TPR; ++t) {
+                    mean[j][r * TPR + t] = m;
+                    rstd[j][r * TPR + t] = rs;
+                }
+            }
     } else if constexpr (op.alias_in) {
         lds_barrier();
     }
 
     prof_mark(a, N_OPS, I, 2);
     // ---- epilogue: GroupNorm affine -> Mish -> + cond / + residual, written as the next conv's planes.
-    // LDS reads of every column tile first (statistics, residual), then the arithmetic, then the writes.
-    f32x4 v[NC];
-    u32x2 rp[NC][P];
+    // LDS reads of every tile first (residual), then the arithmetic, then the writes.
+    f32x4 v[NTW][NCW];
+    u32x2 rp[NTW][NCW][P];
 #pragma unroll
-    for (int cc = 0; cc < NC; ++cc) {
-        v[cc] = acc[cc];
-        if constexpr (EPI == FE_GN_RES) {
-            const char *s = sm + op.res.off + cr[cc] * op.res.rowB + co[cc] * op.res.cs + 2 * n0;
+    for (int j = 0; j < NTW; ++j)
 #pragma unroll
-            for (int pl = 0; pl < P; ++pl) rp[cc][pl] = *reinterpret_cast<const u32x2 *>(s + pl * PLB);
-        }
-    }
-    // GroupNorm affine in log2 units: z = ((x - mean) rstd gamma + beta) log2 e
-    const f32x2 gl0 = lo2(gw) * kLog2e, gl1 = hi2(gw) * kLog2e, bl0 = lo2(gb) * kLog2e, bl1 = hi2(gb) * kLog2e;
+        for (int cc = 0; cc < NCW; ++cc) {
+            v[j][cc] = acc[j][cc];
+            if constexpr (EPI == FE_GN_RES) {
+                const char *s = sm + op.res.off + cr[cc] * op.res.rowB + co[cc] * op.res.cs + 2 * n0[j];
 #pragma unroll
-    for (int cc = 0; cc < NC; ++cc) {
-        if constexpr (GN) {
-            const f32x2 rr = {rstd[cc], rstd[cc]}, mr = {-mean[cc] * rstd[cc], -mean[cc] * rstd[cc]};
-            const f32x2 y0 = mish2_log2(fma2(fma2(lo2(v[cc]), rr, mr), gl0, bl0));
-            const f32x2 y1 = mish2_log2(fma2(fma2(hi2(v[cc]), rr, mr), gl1, bl1));
-            v[cc] = f32x4{y0[0], y0[1], y1[0], y1[1]};
-        }
-        if constexpr (EPI == FE_GN_COND) {
-            const bool masked = cr[cc] >= R / 2;
-            f32x4 cv = masked ? cv1 : cv0;
-            if (!masked && a.cp && a.cp_stride) {
-                const int64_t cand = cand0 + cr[cc];
-                if (cand < a.batch) cv = cv + ldg4(a.cp + (size_t)cand * a.cp_stride + pp.cond_off + n0);
+                for (int pl = 0; pl < P; ++pl) rp[j][cc][pl] = *reinterpret_cast<const u32x2 *>(s + pl * PLB);
             }
-            v[cc] = v[cc] + cv;
-        } else if constexpr (EPI == FE_GN_RES) {
-            v[cc] = v[cc] + join4<P>(rp[cc]);
+        }
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+        // GroupNorm affine in log2 units: z = ((x - mean) rstd gamma + beta) log2 e
+        const f32x2 gl0 = lo2(gw[j]) * kLog2e, gl1 = hi2(gw[j]) * kLog2e;
+        const f32x2 bl0 = lo2(gb[j]) * kLog2e, bl1 = hi2(gb[j]) * kLog2e;
+#pragma unroll
+        for (int cc = 0; cc < NCW; ++cc) {
+            if constexpr (GN) {
+                const float r = rstd[j][cc], mr = -mean[j][cc] * r;
+                const f32x2 rr = {r, r}, mm = {mr, mr};
+                const f32x2 y0 = mish2_log2(fma2(fma2(lo2(v[j][cc]), rr, mm), gl0, bl0));
+                const f32x2 y1 = mish2_log2(fma2(fma2(hi2(v[j][cc]), rr, mm), gl1, bl1));
+                v[j][cc] = f32x4{y0[0], y0[1], y1[0], y1[1]};
+            }
+            if constexpr (EPI == FE_GN_COND) {
+                const bool masked = cr[cc] >= R / 2;
+                f32x4 cv = masked || !shared_cp ? cv1[j] : cv1[j] + cvs[j];
+                if (!masked && a.cp && a.cp_stride) {
+                    const int64_t cand = cand0 + cr[cc];
+                    if (cand < a.batch) cv = cv + ldg4(a.cp + (size_t)cand * a.cp_stride + pp.cond_off + n0[j]);
+                }
+                v[j][cc] = v[j][cc] + cv;
+            } else if constexpr (EPI == FE_GN_RES) {
+                v[j][cc] = v[j][cc] + join4<P>(rp[j][cc]);
+            }
         }
     }
     if constexpr (EPI == FE_EPS) {  // the net's output (cout = d): fp32 for the update
         float *E = reinterpret_cast<float *>(sm + ProgOf<P, R, H>::v.e_off);
 #pragma unroll
-        for (int cc = 0; cc < NC; ++cc)
+        for (int cc = 0; cc < NCW; ++cc)
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-                if (n0 + e < a.d) E[(cr[cc] * H + co[cc]) * a.d + n0 + e] = v[cc][e];
+                if (n0[0] + e < a.d) E[(cr[cc] * H + co[cc]) * a.d + n0[0] + e] = v[0][cc][e];
     } else {
 #pragma unroll
-        for (int cc = 0; cc < NC; ++cc) {
-            u32x2 pk[P];
-            split4<P>(v[cc], pk);
-            char *dst = sm + op.out.off + cr[cc] * op.out.rowB + co[cc] * op.out.cs + 2 * n0;
+        for (int j = 0; j < NTW; ++j)
 #pragma unroll
-            for (int pl = 0; pl < P; ++pl) *reinterpret_cast<u32x2 *>(dst + pl * PLB) = pk[pl];
-            if constexpr (op.spill) {  // the skip tensor as the LDS holds it (fp16), or its fp32 value (re-split on
-                                       // restore); restore_op reads it back in this same lane (program order)
-                const size_t e = ((size_t)(row0 + cr[cc]) * op.out.L + co[cc]) * op.out.C + n0;
-                if constexpr (P == 1)
-                    *reinterpret_cast<u32x2 *>(a.scratch + 2 * e) = pk[0];
-                else
-                    *reinterpret_cast<f32x4 *>(a.scratch + 4 * e) = v[cc];
+            for (int cc = 0; cc < NCW; ++cc) {
+                u32x2 pk[P];
+                split4<P>(v[j][cc], pk);
+                char *dst = sm + op.out.off + cr[cc] * op.out.rowB + co[cc] * op.out.cs + 2 * n0[j];
+#pragma unroll
+                for (int pl = 0; pl < P; ++pl) *reinterpret_cast<u32x2 *>(dst + pl * PLB) = pk[pl];
+                if constexpr (op.spill) {  // the skip tensor as the LDS holds it (fp16), or its fp32 value (re-split
+                                           // on restore); restore_op reads it back in this same lane (program order)
+                    const size_t e = ((size_t)(row0 + cr[cc]) * op.out.L + co[cc]) * op.out.C + n0[j];
+                    if constexpr (P == 1)
+                        *reinterpret_cast<u32x2 *>(a.scratch + 2 * e) = pk[0];
+                    else
+                        *reinterpret_cast<f32x4 *>(a.scratch + 4 * e) = v[j][cc];
+                }
             }
-        }
         zero_halo<P, R, PLB, op.out.off, op.out.rowB, op.out.cs, op.out.C>();
     }
 }
@@ -691,32 +739,37 @@ MPCD_DEV void restore_op(const FArgs &a, int64_t row0)
     extern __shared__ __attribute__((aligned(16))) char sm[];
     using G = OpGeo<P, R, H, I>;
     constexpr COp op = G::op;
-    constexpr int PLB = ProgOf<P, R, H>::v.plb;
+    constexpr int PLB = ProgOf<P, R, H>::v.plb, NTW = G::NTW, NCW = G::NCW;
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int col = lane & 15, q = lane >> 4;
-    int nt, t0, par;
-    wave_tiles<P, R, H, I>(wave, nt, t0, par);
-    const int n0 = nt * 16 + 4 * q;
-    u32x2 pk[G::NC][P];
-    int cr[G::NC], co[G::NC];
+    int nt0, t0, par;
+    wave_tiles<P, R, H, I>(wave, nt0, t0, par);
+    u32x2 pk[NTW][NCW][P];
+    int cr[NCW], co[NCW];
 #pragma unroll
-    for (int cc = 0; cc < G::NC; ++cc) {  // every load in flight before the first LDS write
+    for (int cc = 0; cc < NCW; ++cc) {
         const int c = (t0 + cc) * 16 + col;
         cr[cc] = c >> G::lsh;
         co[cc] = c & (op.lout - 1);
-        const size_t e = ((size_t)(row0 + cr[cc]) * op.out.L + co[cc]) * op.out.C + n0;
-        if constexpr (P == 1) {
-            pk[cc][0] = *reinterpret_cast<const u32x2 *>(a.scratch + 2 * e);
-        } else {
-            split4<P>(*reinterpret_cast<const f32x4 *>(a.scratch + 4 * e), pk[cc]);
+    }
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)  // every load in flight before the first LDS write
+#pragma unroll
+        for (int cc = 0; cc < NCW; ++cc) {
+            const size_t e = ((size_t)(row0 + cr[cc]) * op.out.L + co[cc]) * op.out.C + (nt0 + j) * 16 + 4 * q;
+            if constexpr (P == 1)
+                pk[j][cc][0] = *reinterpret_cast<const u32x2 *>(a.scratch + 2 * e);
+            else
+                split4<P>(*reinterpret_cast<const f32x4 *>(a.scratch + 4 * e), pk[j][cc]);
         }
-    }
 #pragma unroll
-    for (int cc = 0; cc < G::NC; ++cc) {
-        char *dst = sm + op.out.off + cr[cc] * op.out.rowB + co[cc] * op.out.cs + 2 * n0;
+    for (int j = 0; j < NTW; ++j)
 #pragma unroll
-        for (int pl = 0; pl < P; ++pl) *reinterpret_cast<u32x2 *>(dst + pl * PLB) = pk[cc][pl];
-    }
+        for (int cc = 0; cc < NCW; ++cc) {
+            char *dst = sm + op.out.off + cr[cc] * op.out.rowB + co[cc] * op.out.cs + 2 * ((nt0 + j) * 16 + 4 * q);
+#pragma unroll
+            for (int pl = 0; pl < P; ++pl) *reinterpret_cast<u32x2 *>(dst + pl * PLB) = pk[j][cc][pl];
+        }
     zero_halo<P, R, PLB, op.out.off, op.out.rowB, op.out.cs, op.out.C>();
 }
 
@@ -745,8 +798,7 @@ __global__ __launch_bounds__(FT) void unet_fused_kernel(const FArgs a)
     extern __shared__ __attribute__((aligned(16))) char sm[];
     constexpr Prog pg = ProgOf<P, R, H>::v;
     static_assert(pg.ok, "fused U-Net program does not fit this (P, R, H)");
-    constexpr int RC = R / 2, NCB = R * H / 64, PLB = pg.plb;
-    static_assert(NCB >= 2 && NCB % 2 == 0, "R * H / 64 column tiles per wave must be even");
+    constexpr int RC = R / 2, PLB = pg.plb;
     const int tid = threadIdx.x;
     const int64_t cand0 = (int64_t)blockIdx.x * RC, row0 = (int64_t)blockIdx.x * R;
     const int d = a.d;
@@ -813,13 +865,13 @@ struct Cfg {
     int P, R, H;
 };
 // the instantiated configurations (the LDS of R rows fits one CU: static_assert in the kernel)
-constexpr Cfg kCfgs[] = {{1, 4, 64}, {3, 4, 32}, {1, 8, 32}, {3, 2, 64}};
+constexpr Cfg kCfgs[] = {{1, 4, 64}, {3, 4, 32}, {1, 8, 32}, {3, 2, 64}, {1, 2, 64}};
 
 const Prog *prog_of(int P, int R, int H)
 {
 #define C_(p, r, h) \
     if (P == p && R == r && H == h) return &ProgOf<p, r, h>::v;
-    C_(1, 4, 64) C_(3, 4, 32) C_(1, 8, 32) C_(3, 2, 64)
+    C_(1, 4, 64) C_(3, 4, 32) C_(1, 8, 32) C_(3, 2, 64) C_(1, 2, 64)
 #undef C_
     return nullptr;
 }
@@ -838,7 +890,7 @@ hipError_t launch_any(int P, int R, int H, const FArgs &fa, unsigned grid, hipSt
 {
 #define C_(p, r, h) \
     if (P == p && R == r && H == h) return launch_cfg<p, r, h>(fa, grid, st);
-    C_(1, 4, 64) C_(3, 4, 32) C_(1, 8, 32) C_(3, 2, 64)
+    C_(1, 4, 64) C_(3, 4, 32) C_(1, 8, 32) C_(3, 2, 64) C_(1, 2, 64)
 #undef C_
     return hipErrorInvalidValue;
 }
@@ -918,11 +970,11 @@ size_t unet_fused_scratch_bytes(const UnetFusedPlan &pl, int64_t batch)
 int unet_fused_rows_per_wg(const UnetFusedPlan &pl) { return pl.R; }
 int unet_fused_n_ops(const UnetFusedPlan &pl) { return pl.prog->n; }
 int unet_fused_prof_wgs() { return kProfWgs; }
-void unet_fused_op_info(const UnetFusedPlan &pl, int i, int32_t out[6])
+void unet_fused_op_info(const UnetFusedPlan &pl, int i, int32_t out[8])
 {
     const COp &o = pl.prog->ops[i];
-    const int32_t v[6] = {o.kind, o.epi, o.cinp, o.cout, o.lout, o.kc};
-    for (int k = 0; k < 6; ++k) out[k] = v[k];
+    const int32_t v[8] = {o.kind, o.epi, o.cinp, o.cout, o.lout, o.kc, 1 << o.ntw_sh, o.ncw};
+    for (int k = 0; k < 8; ++k) out[k] = v[k];
 }
 
 hipError_t unet_fused_step(const UnetFusedPlan &pl, const UnetFusedStep &s, hipStream_t st)

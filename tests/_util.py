@@ -37,6 +37,12 @@ def assert_traj_close(got, ref, rel=REL_TRAJ, abs_elem=ABS_ELEM, what=""):
     return tr.max(), el.max()
 
 
+# elementwise bar of an ill-conditioned chain (unclamped DDIM): this multiple of the oracle's own spread. Another
+# fp32-accurate implementation (split-bf16 GEMMs, its own reduction orders in the GroupNorm statistics) lands a
+# small multiple of that one-perturbation sample away; the trajectory bar (1e-4 relative) is not relaxed.
+SPREAD_X = 8
+
+
 def oracle_sensitivity(run):
     """Elementwise spread of the oracle itself when every Linear/Conv/GroupNorm rounds from fp64 instead of
     fp32 (a 1-ulp-level perturbation). Unclamped DDIM is ill-conditioned (x0 = a*x - b*eps with a, b up to
