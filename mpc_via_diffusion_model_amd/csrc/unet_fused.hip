@@ -315,14 +315,36 @@ MPCD_DEV float xor32_sum(float v)
     return __builtin_bit_cast(float, own) + __builtin_bit_cast(float, other);
 }
 // sum over a (row segment, GroupNorm group): SEG columns (8 or 16 lanes of one DPP row) x the group's lane
-// quarters (QMASK + 1 of them: 1, 2 or 4); every lane of the group gets the total
+// quarters (QMASK + 1 of them: 1, 2 or 4); every lane of the group gets the total. N independent sums step by
+// step, so the DPP / permlane latencies of one chain hide behind the others.
+template <int SEG, int QMASK, int N>
+MPCD_DEV void group_sum_n(float (&v)[N])
+{
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = dpp_add<0xB1>(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = dpp_add<0x4E>(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = dpp_add<0x141>(v[i]);
+    if constexpr (SEG == 16) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] = dpp_add<0x140>(v[i]);
+    }
+    if constexpr (QMASK >= 1) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] = xor16_sum(v[i]);
+    }
+    if constexpr (QMASK >= 3) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] = xor32_sum(v[i]);
+    }
+}
 template <int SEG, int QMASK>
 MPCD_DEV float group_sum(float v)
 {
-    v = seg_sum<SEG>(v);
-    if constexpr (QMASK >= 1) v = xor16_sum(v);
-    if constexpr (QMASK >= 3) v = xor32_sum(v);
-    return v;
+    float a[1] = {v};
+    group_sum_n<SEG, QMASK, 1>(a);
+    return a[0];
 }
 
 // packed fp32 (v_pk_fma / v_pk_mul / v_pk_add: two lanes' worth per 4-cycle issue; the epilogue is VALU-bound)
@@ -632,14 +654,23 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
         constexpr int L = op.lout, SEG = L < 16 ? L : 16, TPR = L > 16 ? L / 16 : 1;  // column tiles per row
         constexpr float inv_n = 1.0f / (float)(L << op.cpg_sh);
         static_assert(NCW % TPR == 0, "a wave's column tiles are whole rows");
+        constexpr int NR = NCW / TPR, NS = NTW * NR;  // (n-tile, row) sums of the wave, reduced side by side
+        float s1[NS], s2[NS];
 #pragma unroll
         for (int j = 0; j < NTW; ++j)
 #pragma unroll
-            for (int r = 0; r < NCW / TPR; ++r) {
+            for (int r = 0; r < NR; ++r) {
                 f32x2 p1 = lo2(acc[j][r * TPR]) + hi2(acc[j][r * TPR]);
 #pragma unroll
                 for (int t = 1; t < TPR; ++t) p1 += lo2(acc[j][r * TPR + t]) + hi2(acc[j][r * TPR + t]);
-                const float m = group_sum<SEG, QMASK>(p1[0] + p1[1]) * inv_n;
+                s1[j * NR + r] = p1[0] + p1[1];
+            }
+        group_sum_n<SEG, QMASK, NS>(s1);
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const float m = s1[j * NR + r] * inv_n;
                 const f32x2 mm = {-m, -m};
                 f32x2 p2 = {0.f, 0.f};
 #pragma unroll
@@ -647,7 +678,14 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
                     const f32x2 d0 = lo2(acc[j][r * TPR + t]) + mm, d1 = hi2(acc[j][r * TPR + t]) + mm;
                     p2 = fma2(d1, d1, fma2(d0, d0, p2));
                 }
-                const float rs = rsqrt_nr(group_sum<SEG, QMASK>(p2[0] + p2[1]) * inv_n + 1e-5f);
+                s2[j * NR + r] = p2[0] + p2[1];
+            }
+        group_sum_n<SEG, QMASK, NS>(s2);
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const float m = s1[j * NR + r] * inv_n, rs = rsqrt_nr(s2[j * NR + r] * inv_n + 1e-5f);
 #pragma unroll
                 for (int t = 0; t < TPR; ++t) {
                     mean[j][r * TPR + t] = m;
