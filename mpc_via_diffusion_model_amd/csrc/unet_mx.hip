@@ -513,10 +513,11 @@ __device__ __forceinline__ void conv_mx_body(const ConvMK2 &as)
                         const float scale = rstd * gw_t[e];
                         const float shift = -scale * mean + gb_t[e];
                         v[e] = mish(raw[e] * scale + shift);
-                        // Keep each element's Mish in scalar VALU ops: when hipcc (ROCm 7.2) packs the four
-                        // elements into v_pk_{mul,fma}_f32, GroupNorm layers gave wrong, run-to-run varying rows
-                        // whenever two workgroups shared a CU (tests/test_gpu_unet_bench_sizes.py); this empty
-                        // register fence after every element removes them at ~2 % of the kernel's time.
+                        // Keep each element's Mish in scalar VALU ops. Packed by hipcc's SLP vectorizer (ROCm
+                        // 7.2), the epilogue reads v_rcp_f32 results with v_pk_fma_f32 one wait state later (432
+                        // sites), and those builds give wrong conv outputs on the GPU; the same code without SLP
+                        // packing is exact (profiles/r3_hazard_ab.txt, tests/test_isa.py keeps the U-Net kernels
+                        // free of the pattern). This empty register fence per element costs ~2 % of the kernel.
 #ifndef MPCD_MX_NO_FENCE
                         asm volatile("" : "+v"(v[e]));
 #endif

@@ -1,0 +1,93 @@
+"""CPU checks of the gfx950 code libmpcd.so ships (no GPU): two code-generation pitfalls this build hit.
+
+1. Packed-math reads of transcendental results ("Codegen hazards"). With the GroupNorm+Mish
+   epilogue of csrc/unet_mx.hip SLP-packed by hipcc, the conv kernels gave wrong outputs on the GPU
+   (tests/test_gpu_unet_bench_sizes.py, bit-identity across tilings, failed with -DMPCD_MX_NO_FENCE and passed
+   with the fence or with -fno-slp-vectorize: tools/hazard_ab.sh, profiles/r3_hazard_ab.txt). The only code
+   difference: 432 sites where a v_pk_fma_f32 reads a v_rcp_f32 result one wait state after it. The U-Net
+   kernels must keep every packed reader of a transcendental result at >= 2 wait states.
+2. `__builtin_bit_cast` of an element of a builtin's ext-vector result reads element 0 (clang, ROCm 7.2):
+   the permlane-swap reductions of csrc/unet_fused.hip copy the element to a scalar first."""
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB = os.path.join(ROOT, "mpc_via_diffusion_model_amd", "libmpcd.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+HIPCC = "/opt/rocm/bin/hipcc"
+sys.path.insert(0, os.path.join(ROOT, "tools", "isa"))
+
+
+def _disassemble(tmp_path):
+    objdump = os.path.join(LLVM, "llvm-objdump")
+    if not (os.path.exists(LIB) and os.path.exists(objdump)):
+        pytest.skip("libmpcd.so or llvm-objdump not present")
+    so = tmp_path / "libmpcd.so"
+    shutil.copy(LIB, so)
+    subprocess.run([objdump, "--offloading", str(so)], cwd=tmp_path, check=True, capture_output=True)
+    text = []
+    for co in sorted(glob.glob(str(tmp_path / "libmpcd.so.*gfx950"))):
+        r = subprocess.run([objdump, "-d", co], check=True, capture_output=True, text=True)
+        text.append(r.stdout)
+    assert text, "no gfx950 code object in libmpcd.so"
+    return "\n".join(text).splitlines()
+
+
+def test_unet_kernels_keep_packed_reads_of_transcendentals_two_wait_states_away(tmp_path):
+    import trans_hazard as th
+    sites = th.scan(_disassemble(tmp_path))
+    unet = [s for s in sites if s[0] and ("conv_mx_kernel" in s[0] or "unet_fused_kernel" in s[0])]
+    assert any("unet_fused_kernel" in s[0] for s in unet), "fused U-Net kernel not found in the code object"
+    packed = [s for s in unet if s[4]]
+    close = [s for s in packed if s[3] < 2]
+    assert not close, f"{len(close)} packed reads of a transcendental result under 2 wait states: {close[:3]}"
+    assert packed, "the fused U-Net's packed Mish should read exp / rcp results (pattern not found: scan broken?)"
+
+
+def test_scan_finds_the_one_wait_state_pattern():
+    import trans_hazard as th
+    asm = ["_Z1kv:", "  v_rcp_f32_e32 v25, v25", "  s_nop 0", "  v_pk_fma_f32 v[24:25], v[24:25], -2.0, 1.0",
+           "  v_rcp_f32_e32 v27, v27", "  s_nop 1", "  v_pk_fma_f32 v[26:27], v[26:27], -2.0, 1.0",
+           "  v_exp_f32_e32 v30, v30", "  v_add_f32_e32 v31, v30, v30"]
+    sites = th.scan(asm)
+    assert [(s[3], s[4]) for s in sites] == [(1, True), (2, True), (0, False)]
+
+
+def test_bit_cast_of_builtin_vector_element_reads_element_zero(tmp_path):
+    """Evidence for the csrc/unet_fused.hip xor16_sum / xor32_sum workaround: r[0] + bit_cast(r[1]) compiles to
+    r[0] + r[0]; copying r[1] to an unsigned first keeps both results of the swap."""
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not present")
+    src = tmp_path / "k.hip"
+    src.write_text(
+        "#include <hip/hip_runtime.h>\n"
+        "__global__ void bad(float *o, const float *in) {\n"
+        "  const unsigned u = __builtin_bit_cast(unsigned, in[threadIdx.x]);\n"
+        "  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);\n"
+        "  o[threadIdx.x] = __builtin_bit_cast(float, r[0]) + __builtin_bit_cast(float, r[1]);\n"
+        "}\n"
+        "__global__ void good(float *o, const float *in) {\n"
+        "  const unsigned u = __builtin_bit_cast(unsigned, in[threadIdx.x]);\n"
+        "  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);\n"
+        "  const unsigned a = r[0], b = r[1];\n"
+        "  o[threadIdx.x] = __builtin_bit_cast(float, a) + __builtin_bit_cast(float, b);\n"
+        "}\n")
+    out = tmp_path / "k.s"
+    subprocess.run([HIPCC, "-O3", "--offload-arch=gfx950", "--cuda-device-only", "-S", "-o", str(out), str(src)],
+                   check=True, capture_output=True)
+    asm = out.read_text()
+
+    def adds(kernel):
+        body = asm.split(f"{kernel}:", 1)[1].split("s_endpgm", 1)[0]
+        return [ln.split()[1:] for ln in body.splitlines() if ln.strip().startswith("v_add_f32")]
+
+    (bad,) = adds("_Z3badPfPKf")
+    (good,) = adds("_Z4goodPfPKf")
+    assert bad[1].rstrip(",") == bad[2], f"the miscompile is gone ({bad}): the workaround can be dropped"
+    assert good[1].rstrip(",") != good[2], good
