@@ -53,10 +53,11 @@ PEAK_FP32 = 157.3e12      # MI355X dense fp32 MFMA / vector peak, FLOP/s (MI355X
 PEAK_BF16 = 2516.6e12     # MI355X dense bf16 / fp16 MFMA peak: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz
 PMC_FILES = {("cfg2", "f32"): os.path.join(ROOT, "profiles", "r1_pmc_mlp_sampler.json"),
              ("cfg2", "f32x3"): os.path.join(ROOT, "profiles", "r2_pmc_mlp_x3.json"),
-             # U-Net: HBM bytes of one noise-net forward (every conv launch, PMC FETCH_SIZE x2 + WRITE_SIZE) at B
-             ("cfg3", "f32x3"): os.path.join(ROOT, "profiles", "r2_unet_roofline_cfg3.json"),
-             ("cfg4", "f32x3"): os.path.join(ROOT, "profiles", "r2_unet_roofline_cfg4.json"),
-             ("cfg5", "f16"): os.path.join(ROOT, "profiles", "r2_unet_roofline_cfg5.json")}
+             # U-Net: HBM bytes of one noise-net forward (the fused launch of one denoise step, PMC FETCH_SIZE x2 +
+             # WRITE_SIZE, tools/unet_roofline.py) at B
+             ("cfg3", "f32x3"): os.path.join(ROOT, "profiles", "r3_unet_roofline_cfg3.json"),
+             ("cfg4", "f32x3"): os.path.join(ROOT, "profiles", "r3_unet_roofline_cfg4.json"),
+             ("cfg5", "f16"): os.path.join(ROOT, "profiles", "r3_unet_roofline_cfg5.json")}
 
 
 def _rank_env():
@@ -227,23 +228,28 @@ def main():
     else:
         kms = float(np.mean(kernel_ms))
 
-    # strong scaling: what each of 8 GPUs would run (B_total / 8 candidates), measured here on one GPU
-    shard_probe = None
-    if world == 1 and scaling == "strong" and not unet and cfg["B"] % 8 == 0:
-        b8 = cfg["B"] // 8
-        for i in range(5):
-            plan.mpc_step(x0s[i % len(x0s)], system, b8, w=0.01, sample_fn=cfg["sampler"], ddim_steps=cfg["ddim_steps"],
-                          seed=100 + i)
-        torch.cuda.synchronize()
-        t1, n1 = time.perf_counter(), max(steps, 20)
-        for i in range(n1):
-            plan.mpc_step(x0s[i % len(x0s)], system, b8, w=0.01, sample_fn=cfg["sampler"], ddim_steps=cfg["ddim_steps"],
-                          seed=200 + i)
-        torch.cuda.synchronize()
-        el1 = time.perf_counter() - t1
-        shard_probe = {"candidates": b8, "value": b8 * n1 / el1, "ms_per_step": 1e3 * el1 / n1,
-                       "note": f"one GPU running the B_total/8 = {b8}-candidate shard each of 8 GPUs gets under strong "
-                               "scaling (before the exchange); x8 is the compute-only 8-GPU bound"}
+    # strong scaling: the shard each of P = 2, 4, 8 GPUs gets (B_total / P candidates), measured here on one GPU;
+    # (ms_per_step at B_total) / (ms_per_step at B_total / P) is the compute-only P-GPU speedup bound
+    shard_probe = []
+    if world == 1 and scaling == "strong":
+        ms_full = 1e3 * elapsed / steps
+        for div in (2, 4, 8):
+            if cfg["B"] % div:
+                continue
+            bs = cfg["B"] // div
+            nw, n1 = (1, max(2, steps // 2)) if unet else (5, max(steps, 20))
+            for i in range(nw):
+                plan.mpc_step(x0s[i % len(x0s)], system, bs, w=0.01, sample_fn=cfg["sampler"],
+                              ddim_steps=cfg["ddim_steps"], seed=100 + i)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for i in range(n1):
+                plan.mpc_step(x0s[i % len(x0s)], system, bs, w=0.01, sample_fn=cfg["sampler"],
+                              ddim_steps=cfg["ddim_steps"], seed=200 + i)
+            torch.cuda.synchronize()
+            el1 = time.perf_counter() - t1
+            shard_probe.append({"gpus": div, "candidates": bs, "steps": n1, "value": bs * n1 / el1,
+                                "ms_per_step": 1e3 * el1 / n1, "speedup_bound": ms_full / (1e3 * el1 / n1)})
 
     if rank == 0:
         total = b_local * world * steps
@@ -254,9 +260,16 @@ def main():
                 cfg["H"] * cfg["d"])
             timed = f"{kname}: the whole denoising loop in one persistent launch (HIP events on the call's stream)"
         else:
-            kname = "conv_mx_kernel<kind,planes,NN,NC> family" if dtype != "f32" else "conv_kernel family"
-            timed = ("one mpcd_sample call: every U-Net conv launch of the loop + the per-step update kernels "
-                     "(HIP events on the call's stream); the convs are >99% of it (profiles/)")
+            form = plan.unet_form(cfg["sampler"])
+            if form["fused"]:
+                kname = "unet_fused_kernel<%d,%d,%d>" % (form["planes"], form["rows_per_workgroup"], cfg["H"])
+                timed = (f"one mpcd_sample call: {n_evals} {kname} launches (per denoise step the whole noise net "
+                         "for both CFG branches + the update, activations in LDS) + the x_T / chain-maxima kernels "
+                         "(HIP events on the call's stream); the fused launches are >99% of it (profiles/)")
+            else:
+                kname = "conv_mx_kernel<kind,planes,NN,NC> family" if dtype != "f32" else "conv_kernel family"
+                timed = ("one mpcd_sample call: every U-Net conv launch of the loop + the per-step update kernels "
+                         "(HIP events on the call's stream); the convs are >99% of it (profiles/)")
         if dtype == "f32x3":
             mac_exec = cfg["mac_row"] if cfg["mac_row"] else cfg["mac"]
             mfma_flops = b_local * 2 * n_evals * mac_exec * 2 * 6   # six bf16 partial products per fp32 MAC
@@ -313,7 +326,11 @@ def main():
             "best_cost_last_step": r.best_cost,
         }
         if shard_probe:
-            out["strong_shard_probe"] = shard_probe
+            out["strong_shard_probe"] = {
+                "note": "one GPU running the B_total/P-candidate shard each of P GPUs gets under strong scaling "
+                        "(before the per-step exchange); speedup_bound = ms_per_step(B_total) / ms_per_step(shard) "
+                        "is the compute-only P-GPU bound",
+                "shards": shard_probe}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_budget)
         else:

@@ -106,6 +106,7 @@ EXPORTS = {
     "mpcd_unet_force_tiling": ([ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
     "mpcd_mlp_force_layout": ([ctypes.c_int32], ctypes.c_int),
     "mpcd_unet_force_path": ([ctypes.c_int32], ctypes.c_int),
+    "mpcd_unet_form": ([ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "mpcd_comm_init_loopback": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64], ctypes.c_int),
     "mpcd_comm_info": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "mpcd_allgather_f32": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p],

@@ -766,6 +766,16 @@ int mpcd_unet_force_path(int32_t path)
     return MPCD_OK;
 }
 
+int mpcd_unet_form(mpcd_ctx *c, int32_t sampler, int32_t out[3])
+{
+    if (!c || !out) return fail(MPCD_EINVAL, "null argument");
+    if (c->desc.kind != MPCD_NET_UNET) return fail(MPCD_EUNSUP, "not a U-Net context");
+    if (sampler < MPCD_DDPM_CFG || sampler > MPCD_DDIM) return fail(MPCD_EINVAL, "bad sampler %d", sampler);
+    if (!c->unet.ready) return fail(MPCD_ESTATE, "U-Net parameters not loaded");
+    unet_form(c->unet, sampler, out);
+    return MPCD_OK;
+}
+
 int mpcd_mlp_force_layout(int32_t layout)
 {
     if (layout < -1 || layout > 2) return fail(MPCD_EINVAL, "layout -1 (auto), 0 (32x8), 1 (16x8) or 2 (16x4)");

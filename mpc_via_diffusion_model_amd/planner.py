@@ -317,6 +317,13 @@ class DiffusionMPC:
                                    self._stream()), "mpcd_eps")
         return ec, eu
 
+    def unet_form(self, sample_fn="ddpm_cfg"):
+        """The U-Net execution form an mpc_step / sample call with this sampler takes (mpcd_unet_form):
+        {"fused": bool, "planes": 0 | 1 | 3, "rows_per_workgroup": R} - the kernel bench.py names."""
+        out = (ctypes.c_int32 * 3)()
+        N.check(self._lib.mpcd_unet_form(self._ctx, self._sampler_id(sample_fn), out), "mpcd_unet_form")
+        return {"fused": bool(out[0]), "planes": int(out[1]), "rows_per_workgroup": int(out[2])}
+
     def last_sample_ms(self):
         ms = ctypes.c_float()
         N.check(self._lib.mpcd_last_sample_ms(self._ctx, ctypes.byref(ms)), "mpcd_last_sample_ms")

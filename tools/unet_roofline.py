@@ -1,9 +1,10 @@
-"""U-Net roofline table from tools/gpu_unet_roofline.sh output (kernel trace + PMC passes).
+"""U-Net roofline table from `tools/gpu.sh upmc:<cfg>` output (kernel trace + PMC passes).
 
     python tools/unet_roofline.py <cfg> <B> <H> <d> <C> <dtype> [out.json]
 
-Takes the LAST noise-net forward of the run (the conv launch sequence repeats with a fixed period once the
-tiling autotune has cached its picks), and per launch reports duration, HBM bytes (2 x FETCH_SIZE +
+Takes the LAST noise-net forward of the run - one unet_fused_kernel launch (the whole net + that step's update)
+on the fused path, or the period of the conv launch sequence (it repeats once the tiling autotune has cached its
+picks) layer by layer - and per launch reports duration, HBM bytes (2 x FETCH_SIZE +
 WRITE_SIZE, x1024: on gfx950 FETCH_SIZE tallies half the bytes of 16-B/lane streaming reads,
 MI355X_MICROARCH.md §HBM) and MFMA busy; per forward the SURVEY §8d algorithmic FLOPs (2 x MAC x rows),
 the executed matrix-core FLOPs (x6 for the split-bf16 net), and the fractions of the MFMA and HBM peaks.
@@ -22,8 +23,15 @@ def mac_fwd(H, d, C):
     return {32: 9122560, 64: 18209152}[H] + 896 * (C - 5) + 224 * H * (d - 1)
 
 
+KERNELS = ("conv_mx_kernel", "unet_fused_kernel")
+
+
+def is_net(name):
+    return any(k in name for k in KERNELS)
+
+
 def conv_rows(path):
-    rows = [r for r in csv.DictReader(open(path)) if "conv_mx_kernel" in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(path)) if is_net(r["Kernel_Name"])]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     return rows
 
@@ -36,7 +44,10 @@ def period(names):
 
 
 def short(k):
-    return k.split("conv_mx_kernel")[1].split("(")[0]
+    for n in KERNELS:
+        if n in k:
+            return n + k.split(n)[1].split("(")[0].replace(" ", "")
+    return k
 
 
 def main(cfg, B, H, d, C, dtype, out=None):
@@ -51,7 +62,7 @@ def main(cfg, B, H, d, C, dtype, out=None):
     ctr = {}
     for i in range(3):
         rows = [r for r in csv.DictReader(open(f"{base}_p{i}/run_counter_collection.csv"))
-                if "conv_mx_kernel" in r["Kernel_Name"]]
+                if is_net(r["Kernel_Name"])]
         per = {}
         for r in rows:
             per.setdefault(int(r["Dispatch_Id"]), {"name": short(r["Kernel_Name"])})
@@ -86,7 +97,9 @@ def main(cfg, B, H, d, C, dtype, out=None):
         "source": "rocprofv3 --kernel-trace (durations) and three --pmc passes (FETCH_SIZE | WRITE_SIZE | "
                   "SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_MFMA, GRBM_GUI_ACTIVE, ...) over tools/unet_perf.py; "
                   "the last noise-net forward of the run",
-        "conv_launches_per_forward": p,
+        "launches_per_forward": p,
+        "form": "fused (one launch per denoise step: the whole net + the update)" if "unet_fused" in names[-1]
+                else "layer by layer (one launch per conv)",
         "forward_ms": round(t * 1e3, 3),
         "algorithmic_flop_per_forward": flop_alg,
         "executed_mfma_flop_per_forward": flop_exec,
@@ -103,9 +116,9 @@ def main(cfg, B, H, d, C, dtype, out=None):
     if out:
         open(out, "w").write(s)
     print(json.dumps({k: v for k, v in res.items() if k != "per_launch"}, indent=1))
-    print(f"{'i':>3} {'kernel':22s} {'us':>8} {'GFLOP':>8} {'mfma':>6} {'MB':>8} {'GB/s':>8} {'hbm':>6} {'busy':>6}")
+    print(f"{'i':>3} {'kernel':30s} {'us':>8} {'GFLOP':>8} {'mfma':>6} {'MB':>8} {'GB/s':>8} {'hbm':>6} {'busy':>6}")
     for r in table:
-        print(f"{r['i']:3d} {r['kernel']:22s} {r['us']:8.1f} {r['mfma_gflop']:8.1f} {r['mfma_frac']:6.3f} {r['hbm_MB']:8.1f} "
+        print(f"{r['i']:3d} {r['kernel']:30s} {r['us']:8.1f} {r['mfma_gflop']:8.1f} {r['mfma_frac']:6.3f} {r['hbm_MB']:8.1f} "
               f"{r['GB_s']:8.1f} {r['hbm_frac']:6.3f} {r['mfma_busy']:6.3f}")
 
 
