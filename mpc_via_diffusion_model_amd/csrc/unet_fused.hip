@@ -41,7 +41,8 @@ namespace {
 
 using namespace mx;
 
-constexpr int FT = 512;     // threads per workgroup (8 waves)
+constexpr int kNtwMax = 2;   // n-tiles per wave a conv may get: 1 preferred (2 everywhere measured slower, DESIGN.md
+                             // §4), 2 where a 4-wave workgroup has more n-tiles than waves
 constexpr int kGroups = 8;  // GroupNorm groups of every 32 / 64 / 128-channel conv (group_norm_n_groups)
 
 enum { FK_SAME5 = 0, FK_DOWN3 = 1, FK_UP4 = 2, FK_PW1 = 3, FK_RESTORE = 4 };
@@ -90,7 +91,7 @@ constexpr int ilog2c(int v)
     return (1 << s) == v ? s : -1;
 }
 
-template <int P, int R, int H, int NTW_MAX>
+template <int P, int R, int H, int W>
 constexpr Prog make_prog()
 {
     Prog pg{};
@@ -146,11 +147,11 @@ constexpr Prog make_prog()
         const bool gn = epi == FE_GN || epi == FE_GN_COND || epi == FE_GN_RES;
         o.cpg_sh = gn ? ilog2c(cout / kGroups) : 0;
         if (gn && (o.cpg_sh < 2 || o.cpg_sh > 4 || o.lout < 8)) pg.ok = 0;
-        // tiling: two n-tiles per wave where the op has them and the columns split evenly, else one; a wave's
+        // tiling: one n-tile per wave where the columns split evenly over the waves, else two; a wave's
         // columns in one UP4 parity, and (GroupNorm) whole rows or one half of a row
         o.ntw_sh = -1;
-        for (int w = (nt >= 2 && NTW_MAX >= 2) ? 1 : 0; w >= 0 && o.ntw_sh < 0; --w) {
-            const int ntg = nt >> w, wc = ntg >= 1 && ntg <= 8 ? 8 / ntg : 0;
+        for (int w = 0; w <= (nt >= 2 && kNtwMax >= 2 ? 1 : 0) && o.ntw_sh < 0; ++w) {
+            const int ntg = nt >> w, wc = ntg >= 1 && ntg <= W ? W / ntg : 0;
             const int ncw = wc && ct % wc == 0 ? ct / wc : 0;
             if (ncw < 1 || (ncw << w) > 4 || (kind == FK_UP4 && (R * lin / 16) % ncw)) continue;
             const int wpr = gn && o.lout > 16 && (ncw * 16) % o.lout ? o.lout / (ncw * 16) : 1;
@@ -235,9 +236,9 @@ constexpr Prog make_prog()
     return pg;
 }
 
-template <int P, int R, int H>
+template <int P, int R, int H, int W>
 struct ProgOf {
-    static constexpr Prog v = make_prog<P, R, H, 1>();
+    static constexpr Prog v = make_prog<P, R, H, W>();
 };
 
 // ---- runtime tables and kernel arguments
@@ -383,9 +384,9 @@ template <int P> struct APre {                          // the next conv's first
     u32x4 A[kDA<P>][kNTW][P];
 };
 
-template <int P, int R, int H, int I>
+template <int P, int R, int H, int W, int I>
 struct OpGeo {  // the wave-independent constants of op I
-    static constexpr COp op = ProgOf<P, R, H>::v.ops[I];
+    static constexpr COp op = ProgOf<P, R, H, W>::v.ops[I];
     static constexpr int NT = 1 << op.nt_sh, NTW = 1 << op.ntw_sh, NCW = op.ncw;
     static constexpr int ntg_sh = op.nt_sh - op.ntw_sh;                // log2 n-tile groups
     static constexpr int lcol = op.kind == FK_UP4 ? op.lin : op.lout;  // columns per row and parity
@@ -414,24 +415,24 @@ MPCD_DEV void load_a(const __amdgpu_buffer_rsrc_t &rs, int par, int nt0, int kc,
 }
 
 // this wave's first n-tile, first column tile and parity (UP4) in op I
-template <int P, int R, int H, int I>
+template <int P, int R, int H, int W, int I>
 MPCD_DEV void wave_tiles(int wave, int &nt0, int &t0, int &par)
 {
-    using G = OpGeo<P, R, H, I>;
+    using G = OpGeo<P, R, H, W, I>;
     nt0 = (wave & ((1 << G::ntg_sh) - 1)) << G::op.ntw_sh;
     t0 = (wave >> G::ntg_sh) * G::NCW;
     par = G::op.kind == FK_UP4 && t0 >= G::tiles_par ? 1 : 0;  // make_prog: NCW divides tiles_par
 }
 
 // issue the first A chunks of op I for this wave (so they land while the previous op's epilogue runs)
-template <int P, int R, int H, int I>
+template <int P, int R, int H, int W, int I>
 MPCD_DEV void prefetch_op(const FArgs &a, int wave, int lane, APre<P> &pre)
 {
-    using G = OpGeo<P, R, H, I>;
+    using G = OpGeo<P, R, H, W, I>;
     if constexpr (G::op.kind != FK_RESTORE) {
         CPtr &pp = reinterpret_cast<CPtr *>((uintptr_t)a.ptrs)[I];
         int nt0, t0, par;
-        wave_tiles<P, R, H, I>(wave, nt0, t0, par);
+        wave_tiles<P, R, H, W, I>(wave, nt0, t0, par);
         const __amdgpu_buffer_rsrc_t rs = weight_rsrc<P>(pp.w, G::wbytes);
 #pragma unroll
         for (int s = 0; s < kDA<P>; ++s)
@@ -441,7 +442,7 @@ MPCD_DEV void prefetch_op(const FArgs &a, int wave, int lane, APre<P> &pre)
 
 // zero the halo positions of a view (every plane, the view's channels): the R + 1 gaps of two positions each,
 // in front of every row and after the last
-template <int P, int R, int PLB, int OFF, int ROWB, int CS, int C>
+template <int P, int R, int FT, int PLB, int OFF, int ROWB, int CS, int C>
 MPCD_DEV void zero_halo()
 {
     extern __shared__ __attribute__((aligned(16))) char sm[];
@@ -454,15 +455,15 @@ MPCD_DEV void zero_halo()
 }
 
 // ---- one conv of the program: GEMM + statistics + epilogue
-template <int P, int R, int H, int I>
+template <int P, int R, int H, int W, int I>
 MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
 {
     extern __shared__ __attribute__((aligned(16))) char sm[];
-    using G = OpGeo<P, R, H, I>;
+    using G = OpGeo<P, R, H, W, I>;
     constexpr COp op = G::op;
     constexpr int NCW = G::NCW, NTW = G::NTW, NT = G::NT, KC = op.kc, KIND = op.kind, EPI = op.epi;
     constexpr int DA = kDA<P>, DB = kDB;
-    constexpr int PLB = ProgOf<P, R, H>::v.plb, N_OPS = ProgOf<P, R, H>::v.n;
+    constexpr int PLB = ProgOf<P, R, H, W>::v.plb, N_OPS = ProgOf<P, R, H, W>::v.n;
     constexpr bool GN = EPI == FE_GN || EPI == FE_GN_COND || EPI == FE_GN_RES;
     static_assert(!(GN && op.alias_in), "GroupNorm ops write a region their GEMM does not read");
     static_assert(EPI != FE_EPS || NTW == 1, "the eps conv has one n-tile");
@@ -470,7 +471,7 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int col = lane & 15, q = lane >> 4;
     int nt0, t0, par;
-    wave_tiles<P, R, H, I>(wave, nt0, t0, par);
+    wave_tiles<P, R, H, W, I>(wave, nt0, t0, par);
     int n0[NTW];  // first of the lane's 4 output channels, per n-tile of the wave
 #pragma unroll
     for (int j = 0; j < NTW; ++j) n0[j] = (nt0 + j) * 16 + 4 * q;
@@ -599,7 +600,7 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
 #pragma unroll
         for (int cc = 0; cc < NCW; ++cc) acc[j][cc] = acc[j][cc] + bias[j];
 
-    if constexpr (I + 1 < N_OPS) prefetch_op<P, R, H, I + 1>(a, wave, lane, pre);  // lands during the epilogue
+    if constexpr (I + 1 < N_OPS) prefetch_op<P, R, H, W, I + 1>(a, wave, lane, pre);  // lands during the epilogue
     prof_mark(a, N_OPS, I, 1);
     // ---- GroupNorm statistics per (row, group): a group's channels are 1, 2 or 4 lane quarters of one n-tile,
     // its columns the DPP-row lanes of the wave's tiles in that row. Exact two-pass (mean, then the centred sum of
@@ -610,7 +611,7 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
         // a row spans two waves (the wave's NCW tiles are one half of it): per-wave partial sums through LDS,
         // added in wave order; two barriers per op
         constexpr float inv_n = 1.0f / (float)(op.lout << op.cpg_sh);
-        float *st = reinterpret_cast<float *>(sm + ProgOf<P, R, H>::v.stat_off);  // [S1 | S2][row][group][half]
+        float *st = reinterpret_cast<float *>(sm + ProgOf<P, R, H, W>::v.stat_off);  // [S1 | S2][row][group][half]
         const int row = cr[0], half = (t0 / NCW) & 1;
         const bool leader = col == 0 && (q & QMASK) == 0;
         int slot[NTW];
@@ -740,7 +741,7 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
         }
     }
     if constexpr (EPI == FE_EPS) {  // the net's output (cout = d): fp32 for the update
-        float *E = reinterpret_cast<float *>(sm + ProgOf<P, R, H>::v.e_off);
+        float *E = reinterpret_cast<float *>(sm + ProgOf<P, R, H, W>::v.e_off);
 #pragma unroll
         for (int cc = 0; cc < NCW; ++cc)
 #pragma unroll
@@ -765,23 +766,23 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
                         *reinterpret_cast<f32x4 *>(a.scratch + 4 * e) = v[j][cc];
                 }
             }
-        zero_halo<P, R, PLB, op.out.off, op.out.rowB, op.out.cs, op.out.C>();
+        zero_halo<P, R, 64 * W, PLB, op.out.off, op.out.rowB, op.out.cs, op.out.C>();
     }
 }
 
 // skip tensor back from the scratch into its LDS view: the RESTORE op carries the spilling conv's tile
 // geometry (n-tiles, column tiles per wave, length), so every lane reads back exactly the elements it stored
-template <int P, int R, int H, int I>
+template <int P, int R, int H, int W, int I>
 MPCD_DEV void restore_op(const FArgs &a, int64_t row0)
 {
     extern __shared__ __attribute__((aligned(16))) char sm[];
-    using G = OpGeo<P, R, H, I>;
+    using G = OpGeo<P, R, H, W, I>;
     constexpr COp op = G::op;
-    constexpr int PLB = ProgOf<P, R, H>::v.plb, NTW = G::NTW, NCW = G::NCW;
+    constexpr int PLB = ProgOf<P, R, H, W>::v.plb, NTW = G::NTW, NCW = G::NCW;
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int col = lane & 15, q = lane >> 4;
     int nt0, t0, par;
-    wave_tiles<P, R, H, I>(wave, nt0, t0, par);
+    wave_tiles<P, R, H, W, I>(wave, nt0, t0, par);
     u32x2 pk[NTW][NCW][P];
     int cr[NCW], co[NCW];
 #pragma unroll
@@ -808,33 +809,34 @@ MPCD_DEV void restore_op(const FArgs &a, int64_t row0)
 #pragma unroll
             for (int pl = 0; pl < P; ++pl) *reinterpret_cast<u32x2 *>(dst + pl * PLB) = pk[j][cc][pl];
         }
-    zero_halo<P, R, PLB, op.out.off, op.out.rowB, op.out.cs, op.out.C>();
+    zero_halo<P, R, 64 * W, PLB, op.out.off, op.out.rowB, op.out.cs, op.out.C>();
 }
 
-template <int P, int R, int H, int I>
+template <int P, int R, int H, int W, int I>
 MPCD_DEV void run_ops(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
 {
-    constexpr int N_OPS = ProgOf<P, R, H>::v.n;
+    constexpr int N_OPS = ProgOf<P, R, H, W>::v.n;
     if constexpr (I < N_OPS) {
         prof_mark(a, N_OPS, I, 0);
-        if constexpr (ProgOf<P, R, H>::v.ops[I].kind == FK_RESTORE) {
-            restore_op<P, R, H, I>(a, row0);
-            if constexpr (I + 1 < N_OPS) prefetch_op<P, R, H, I + 1>(a, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
+        if constexpr (ProgOf<P, R, H, W>::v.ops[I].kind == FK_RESTORE) {
+            restore_op<P, R, H, W, I>(a, row0);
+            if constexpr (I + 1 < N_OPS) prefetch_op<P, R, H, W, I + 1>(a, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
                                                                      threadIdx.x & 63, pre);
         } else {
-            conv_op<P, R, H, I>(a, cand0, row0, pre);
+            conv_op<P, R, H, W, I>(a, cand0, row0, pre);
         }
         lds_barrier();
         prof_mark(a, N_OPS, I, 3);
-        run_ops<P, R, H, I + 1>(a, cand0, row0, pre);
+        run_ops<P, R, H, W, I + 1>(a, cand0, row0, pre);
     }
 }
 
-template <int P, int R, int H>
-__global__ __launch_bounds__(FT) void unet_fused_kernel(const FArgs a)
+template <int P, int R, int H, int W>
+__global__ __launch_bounds__(64 * W) void unet_fused_kernel(const FArgs a)
 {
+    constexpr int FT = 64 * W;
     extern __shared__ __attribute__((aligned(16))) char sm[];
-    constexpr Prog pg = ProgOf<P, R, H>::v;
+    constexpr Prog pg = ProgOf<P, R, H, W>::v;
     static_assert(pg.ok, "fused U-Net program does not fit this (P, R, H)");
     constexpr int RC = R / 2, PLB = pg.plb;
     const int tid = threadIdx.x;
@@ -842,7 +844,7 @@ __global__ __launch_bounds__(FT) void unet_fused_kernel(const FArgs a)
     const int d = a.d;
     APre<P> pre;
     // the first conv's weights are in flight while x is staged
-    prefetch_op<P, R, H, 0>(a, __builtin_amdgcn_readfirstlane(tid >> 6), tid & 63, pre);
+    prefetch_op<P, R, H, W, 0>(a, __builtin_amdgcn_readfirstlane(tid >> 6), tid & 63, pre);
 
     // ---- stage x (both branches of each candidate) as 8 zero-padded channels, with its 2 + 5 zero positions
     {
@@ -863,7 +865,7 @@ __global__ __launch_bounds__(FT) void unet_fused_kernel(const FArgs a)
     }
     lds_barrier();
 
-    run_ops<P, R, H, 0>(a, cand0, row0, pre);
+    run_ops<P, R, H, W, 0>(a, cand0, row0, pre);
 
     // ---- the denoise update of this step (or the raw eps of both branches, MODE_EPS)
     const float *E = reinterpret_cast<const float *>(sm + pg.e_off);
@@ -900,35 +902,45 @@ __global__ __launch_bounds__(FT) void unet_fused_kernel(const FArgs a)
 // ---- host
 
 struct Cfg {
-    int P, R, H;
+    int P, R, H, W;  // numerics planes, rows per workgroup, horizon, waves per workgroup
 };
 // the instantiated configurations (the LDS of R rows fits one CU: static_assert in the kernel)
-constexpr Cfg kCfgs[] = {{1, 4, 64}, {3, 4, 32}, {1, 8, 32}, {3, 2, 64}, {1, 2, 64}};
+// the first match of (P, H) is the default; MPCD_FUSED_ROWS / MPCD_FUSED_WAVES pick another (experiments)
+// (1, 2, 64, 4): two or three 4-wave workgroups per CU, their barriers independent (cfg5 14.7 ms per CFG evaluation
+// vs 15.3 for one 8-wave workgroup of 4 rows); the split-bf16 nets keep 4-row blocks (their weights, three planes,
+// miss the L2 per block: cfg3 3.98 ms with 2-row blocks vs 3.58)
+#define MPCD_FUSED_CFGS C_(1, 2, 64, 4) C_(3, 4, 32, 8) C_(1, 8, 32, 8) C_(3, 2, 64, 8) C_(1, 4, 64, 8) \
+    C_(1, 2, 64, 8) C_(3, 2, 32, 4)
+constexpr Cfg kCfgs[] = {
+#define C_(p, r, h, w) {p, r, h, w},
+    MPCD_FUSED_CFGS
+#undef C_
+};
 
-const Prog *prog_of(int P, int R, int H)
+const Prog *prog_of(int P, int R, int H, int W)
 {
-#define C_(p, r, h) \
-    if (P == p && R == r && H == h) return &ProgOf<p, r, h>::v;
-    C_(1, 4, 64) C_(3, 4, 32) C_(1, 8, 32) C_(3, 2, 64) C_(1, 2, 64)
+#define C_(p, r, h, w) \
+    if (P == p && R == r && H == h && W == w) return &ProgOf<p, r, h, w>::v;
+    MPCD_FUSED_CFGS
 #undef C_
     return nullptr;
 }
 
-template <int P, int R, int H>
+template <int P, int R, int H, int W>
 hipError_t launch_cfg(const FArgs &fa, unsigned grid, hipStream_t st)
 {
-    constexpr auto kfn = &unet_fused_kernel<P, R, H>;
+    constexpr auto kfn = &unet_fused_kernel<P, R, H, W>;
     if (hipError_t e = allow_max_lds<kfn>(); e != hipSuccess) return e;
-    constexpr size_t lds = ProgOf<P, R, H>::v.lds;
-    hipLaunchKernelGGL(kfn, dim3(grid), dim3(FT), lds, st, fa);
+    constexpr size_t lds = ProgOf<P, R, H, W>::v.lds;
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * W), lds, st, fa);
     return hipGetLastError();
 }
 
-hipError_t launch_any(int P, int R, int H, const FArgs &fa, unsigned grid, hipStream_t st)
+hipError_t launch_any(int P, int R, int H, int W, const FArgs &fa, unsigned grid, hipStream_t st)
 {
-#define C_(p, r, h) \
-    if (P == p && R == r && H == h) return launch_cfg<p, r, h>(fa, grid, st);
-    C_(1, 4, 64) C_(3, 4, 32) C_(1, 8, 32) C_(3, 2, 64) C_(1, 2, 64)
+#define C_(p, r, h, w) \
+    if (P == p && R == r && H == h && W == w) return launch_cfg<p, r, h, w>(fa, grid, st);
+    MPCD_FUSED_CFGS
 #undef C_
     return hipErrorInvalidValue;
 }
@@ -936,7 +948,7 @@ hipError_t launch_any(int P, int R, int H, const FArgs &fa, unsigned grid, hipSt
 }  // namespace
 
 struct UnetFusedPlan {
-    int P = 0, R = 0, H = 0, d = 0;
+    int P = 0, R = 0, H = 0, W = 0, d = 0;
     const Prog *prog = nullptr;
     FPtr *ptrs_dev = nullptr;
     ~UnetFusedPlan()
@@ -964,11 +976,13 @@ UnetFusedPlan *unet_fused_prepare(const mpcd_net_desc &d, const UnetWeights &W, 
     if ((H * d.state_dim) % 4) return no("fused U-Net: H*d must be a multiple of 4");
     if (W.n_layers != 35) return no("fused U-Net: unexpected layer count");
     const Prog *pg = nullptr;
-    int R = 0;
+    int R = 0, Wv = 0;
+    static const int waves = getenv("MPCD_FUSED_WAVES") ? atoi(getenv("MPCD_FUSED_WAVES")) : 0;  // experiments
     for (const Cfg &c : kCfgs)
-        if (c.P == P && c.H == H && (rows_per_wg <= 0 || rows_per_wg == c.R)) {
+        if (c.P == P && c.H == H && (rows_per_wg <= 0 || rows_per_wg == c.R) && (waves <= 0 || waves == c.W)) {
             R = c.R;
-            pg = prog_of(c.P, c.R, c.H);
+            Wv = c.W;
+            pg = prog_of(c.P, c.R, c.H, c.W);
             break;
         }
     if (!pg) return no("fused U-Net: no instantiation for this horizon / numerics / rows per workgroup");
@@ -988,6 +1002,7 @@ UnetFusedPlan *unet_fused_prepare(const mpcd_net_desc &d, const UnetWeights &W, 
     auto *pl = new UnetFusedPlan;
     pl->P = P;
     pl->R = R;
+    pl->W = Wv;
     pl->H = H;
     pl->d = d.state_dim;
     pl->prog = pg;
@@ -1044,5 +1059,5 @@ hipError_t unet_fused_step(const UnetFusedPlan &pl, const UnetFusedStep &s, hipS
     fa.prof = s.prof;
     const int64_t grid = (s.batch + pl.R / 2 - 1) / (pl.R / 2);
     if (grid <= 0 || grid > 0x7fffffff) return hipErrorInvalidValue;
-    return launch_any(pl.P, pl.R, pl.H, fa, (unsigned)grid, st);
+    return launch_any(pl.P, pl.R, pl.H, pl.W, fa, (unsigned)grid, st);
 }
