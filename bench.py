@@ -166,6 +166,7 @@ def main():
                     help="strong (SURVEY §8d: fixed B_total split over the ranks) or weak (B per rank)")
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-shard-probe", action="store_true", help="skip the strong-scaling shard probes (kernel traces)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--dtype", default=None, choices=["f32", "f32x3", "f16"],
                     help="GEMM numerics: exact fp32 MFMA, fp32-accurate split-bf16 MFMA, fp16 operands (U-Net)")
@@ -231,7 +232,7 @@ def main():
     # strong scaling: the shard each of P = 2, 4, 8 GPUs gets (B_total / P candidates), measured here on one GPU;
     # (ms_per_step at B_total) / (ms_per_step at B_total / P) is the compute-only P-GPU speedup bound
     shard_probe = []
-    if world == 1 and scaling == "strong":
+    if world == 1 and scaling == "strong" and not args.no_shard_probe:
         ms_full = 1e3 * elapsed / steps
         for div in (2, 4, 8):
             if cfg["B"] % div:
@@ -262,7 +263,8 @@ def main():
         else:
             form = plan.unet_form(cfg["sampler"])
             if form["fused"]:
-                kname = "unet_fused_kernel<%d,%d,%d>" % (form["planes"], form["rows_per_workgroup"], cfg["H"])
+                kname = "unet_fused_kernel<%d,%d,%d,%d>" % (form["planes"], form["rows_per_workgroup"], cfg["H"],
+                                                            form["waves_per_workgroup"])
                 timed = (f"one mpcd_sample call: {n_evals} {kname} launches (per denoise step the whole noise net "
                          "for both CFG branches + the update, activations in LDS) + the x_T / chain-maxima kernels "
                          "(HIP events on the call's stream); the fused launches are >99% of it (profiles/)")

@@ -350,8 +350,9 @@ int mpcd_unet_force_path(int32_t path);
 /* Which form an mpcd_sample call with this sampler (mpcd_sampler) takes on this context's U-Net under the
  * current mpcd_unet_force_path / MPCD_UNET_FUSED settings: out[0] = 1 whole-network fused launch per denoise
  * step / 0 layer by layer, out[1] = GEMM operand planes (0 exact fp32, 1 fp16, 3 split bf16), out[2] = rows
- * (candidate x CFG branch) per workgroup of the fused launch. MPCD_EUNSUP on an MLP context. */
-int mpcd_unet_form(mpcd_ctx *ctx, int32_t sampler, int32_t out[3]);
+ * (candidate x CFG branch) and out[3] = waves per workgroup of the fused launch. MPCD_EUNSUP on an MLP
+ * context. */
+int mpcd_unet_form(mpcd_ctx *ctx, int32_t sampler, int32_t out[4]);
 #define MPCD_UNET_MAX_CONV_TILINGS 12   /* 6 rows-per-workgroup values x {tiled, persistent} */
 #define MPCD_UNET_MAX_BLOCK_TILINGS 6
 

@@ -766,7 +766,7 @@ int mpcd_unet_force_path(int32_t path)
     return MPCD_OK;
 }
 
-int mpcd_unet_form(mpcd_ctx *c, int32_t sampler, int32_t out[3])
+int mpcd_unet_form(mpcd_ctx *c, int32_t sampler, int32_t out[4])
 {
     if (!c || !out) return fail(MPCD_EINVAL, "null argument");
     if (c->desc.kind != MPCD_NET_UNET) return fail(MPCD_EUNSUP, "not a U-Net context");

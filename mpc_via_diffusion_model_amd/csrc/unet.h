@@ -149,8 +149,9 @@ hipError_t unet_fused_step(const UnetFusedPlan &pl, const UnetFusedStep &s, hipS
 // mpcd_unet_force_path: 0 = automatic, 1 = layer by layer, 2 = fused (error where it does not apply)
 void unet_force_path(int path);
 // the form a sample call of sampler `mode` takes: out = {1 fused / 0 layer by layer, operand planes (0 = fp32
-// FMA, 1 = fp16, 3 = split bf16), rows per workgroup of the fused program (0 when layered)}
-void unet_form(const UnetWeights &W, int mode, int32_t out[3]);
+// FMA, 1 = fp16, 3 = split bf16), rows and waves per workgroup of the fused program (0 when layered)}
+void unet_form(const UnetWeights &W, int mode, int32_t out[4]);
+int unet_fused_waves_per_wg(const UnetFusedPlan &pl);
 
 // mpcd_unet_force_tiling (include/mpcd.h)
 void unet_force_tiling(int conv, int block);

@@ -823,12 +823,13 @@ bool use_fused(const UnetWeights &W, int mode)
 
 void unet_force_path(int path) { g_unet_path.store(path); }
 
-void unet_form(const UnetWeights &W, int mode, int32_t out[3])
+void unet_form(const UnetWeights &W, int mode, int32_t out[4])
 {
     const bool f = use_fused(W, mode);
     out[0] = f ? 1 : 0;
     out[1] = W.planes;
     out[2] = f ? unet_fused_rows_per_wg(*W.fused) : 0;
+    out[3] = f ? unet_fused_waves_per_wg(*W.fused) : 0;
 }
 
 size_t unet_workspace_bytes(const mpcd_net_desc &d, const UnetWeights &W, int mode, int64_t batch, int nb)

@@ -1021,6 +1021,7 @@ size_t unet_fused_scratch_bytes(const UnetFusedPlan &pl, int64_t batch)
 }
 
 int unet_fused_rows_per_wg(const UnetFusedPlan &pl) { return pl.R; }
+int unet_fused_waves_per_wg(const UnetFusedPlan &pl) { return pl.W; }
 int unet_fused_n_ops(const UnetFusedPlan &pl) { return pl.prog->n; }
 int unet_fused_prof_wgs() { return kProfWgs; }
 void unet_fused_op_info(const UnetFusedPlan &pl, int i, int32_t out[8])

@@ -319,10 +319,12 @@ class DiffusionMPC:
 
     def unet_form(self, sample_fn="ddpm_cfg"):
         """The U-Net execution form an mpc_step / sample call with this sampler takes (mpcd_unet_form):
-        {"fused": bool, "planes": 0 | 1 | 3, "rows_per_workgroup": R} - the kernel bench.py names."""
-        out = (ctypes.c_int32 * 3)()
+        {"fused": bool, "planes": 0 | 1 | 3, "rows_per_workgroup": R, "waves_per_workgroup": W} - the kernel
+        bench.py names."""
+        out = (ctypes.c_int32 * 4)()
         N.check(self._lib.mpcd_unet_form(self._ctx, self._sampler_id(sample_fn), out), "mpcd_unet_form")
-        return {"fused": bool(out[0]), "planes": int(out[1]), "rows_per_workgroup": int(out[2])}
+        return {"fused": bool(out[0]), "planes": int(out[1]), "rows_per_workgroup": int(out[2]),
+                "waves_per_workgroup": int(out[3])}
 
     def last_sample_ms(self):
         ms = ctypes.c_float()

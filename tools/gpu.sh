@@ -44,7 +44,7 @@ run_job() {
     trace)
       local w=${arg:-cfg2}
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "gpurun_out/prof/trace_$w" -o run -f csv -- \
-        python3 bench.py --workload "$w" --no-cpu-baseline $BENCH_ARGS > "gpurun_out/prof/trace_$w.log" 2>&1 ;;
+        python3 bench.py --workload "$w" --no-cpu-baseline --no-shard-probe $BENCH_ARGS > "gpurun_out/prof/trace_$w.log" 2>&1 ;;
     pmc)
       local w=${arg:-cfg2} c
       for c in FETCH_SIZE WRITE_SIZE; do
