@@ -205,3 +205,29 @@ def test_data_parallel_loopback_equals_full_batch(kind, shape):
                 assert _rel(g0[n], gf[n]) <= 1e-5, (step, n, _rel(g0[n], gf[n]))
         p0, p1 = ranks[0].state_dict("params"), ranks[1].state_dict("params")
         assert all(torch.equal(p0[n], p1[n]) for n in p0)
+
+
+def test_wide_mlp_step_matches_oracle():
+    """A wider MLP than the sampler covers (base 64, dim_mults (1, 2, 4, 8): 512-wide hidden layers) through the
+    training step: the backward's scratch holds the widest layer (round-2 advisor finding), loss and gradients
+    against the oracle."""
+    from oracle import nets
+    d, H, C, B = 2, 16, 4, 96
+    torch.manual_seed(3)
+    net = nets.ConditionedMLPNet(state_dim=d, horizon=H, context_dim=C, dim=64, dim_mults=(1, 2, 4, 8)).train()
+    tables = osch.buffers("exponential", 100)
+    tr = DiffusionTrainer(NetSpec("mlp", d, H, C, base_dim=64, dim_mults=(1, 2, 4, 8)), net.state_dict(), tables=tables)
+    orc = OracleTrainer(net, tables)
+    g = torch.Generator().manual_seed(4)
+    x0 = torch.rand(B, H, d, generator=g) * 2 - 1
+    ctx = torch.rand(B, C, generator=g) * 2 - 1
+    t, noise, mask = tr.draw(B, (B, H, d), generator=g)
+    ref_loss = orc.train_step(x0, ctx, t, noise, mask)
+    got_loss = tr.train_step(x0, ctx, t, noise, mask)
+    assert abs(got_loss - ref_loss) <= 1e-5 * abs(ref_loss), (got_loss, ref_loss)
+    grads = tr.state_dict("grads")
+    for n, p in orc.net.named_parameters():
+        if float(p.grad.norm()) == 0.0:
+            assert float(grads[n].norm()) == 0.0, n
+            continue
+        assert _rel(grads[n], p.grad) <= 1e-4, (n, _rel(grads[n], p.grad))
