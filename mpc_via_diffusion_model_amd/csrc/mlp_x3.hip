@@ -59,6 +59,12 @@ constexpr int ROWS_MAX = 32;
 #ifndef MPCD_X3_ILV
 #define MPCD_X3_ILV 1
 #endif
+#ifndef MPCD_X3_WF32
+#define MPCD_X3_WF32 0
+#endif
+#ifndef MPCD_X3_IDLE_OOB
+#define MPCD_X3_IDLE_OOB 0
+#endif
 constexpr int THREADS = 64 * MPCD_X3_WAVES;
 constexpr int WAVES = THREADS / 64;
 enum { SPLIT = 0, PAIRED = 1, WIDE8 = 2, PAIR8 = 3 };
@@ -148,6 +154,50 @@ struct WFrag3 {
     u32x4 v[T][KC][3];
 };
 
+// What one wave loads for a layer: per (n-tile, k-chunk) WPL 16-byte pieces per lane — the three bf16
+// planes, or (MPCD_X3_WF32) the 8 fp32 weights as two halves, split into the planes in registers right
+// before the layer (to_planes: the same round-to-nearest-even split the host does, so the MFMA operands
+// are bit-identical) — 4 instead of 6 bytes per weight streamed from L2 every step.
+constexpr int WPL = MPCD_X3_WF32 ? 2 : 3;
+template <int K, int N, int MODE>
+struct WLoad {
+    using F = WFrag3<K, N, MODE>;
+    static constexpr int NT = F::NT, T = F::T, KC = F::KC;
+    u32x4 v[T][KC][WPL];
+};
+
+template <int K, int N, int MODE>
+MPCD_DEV void to_planes(const WLoad<K, N, MODE> &w, WFrag3<K, N, MODE> &f)
+{
+#pragma unroll
+    for (int j = 0; j < WFrag3<K, N, MODE>::T; ++j)
+#pragma unroll
+        for (int kc = 0; kc < WFrag3<K, N, MODE>::KC; ++kc) {
+            if constexpr (WPL == 3) {
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) f.v[j][kc][pl] = w.v[j][kc][pl];
+            } else {
+                u32x2 a0, a1, a2, b0, b1, b2;
+                split3(__builtin_bit_cast(f32x4, w.v[j][kc][0]), a0, a1, a2);
+                split3(__builtin_bit_cast(f32x4, w.v[j][kc][1]), b0, b1, b2);
+                f.v[j][kc][0] = u32x4{a0.x, a0.y, b0.x, b0.y};
+                f.v[j][kc][1] = u32x4{a1.x, a1.y, b1.x, b1.y};
+                f.v[j][kc][2] = u32x4{a2.x, a2.y, b2.x, b2.y};
+            }
+        }
+}
+
+// packed floats per layer (weights, then the N fp32 biases) and layer offsets in the x3 pack
+template <int D0>
+constexpr int wfl(int l) { return WPL * Arch<D0>::K[l] * Arch<D0>::N[l] / 2; }
+template <int D0>
+constexpr int woffx(int l)
+{
+    int o = 0;
+    for (int i = 0; i < l; ++i) o += wfl<D0>(i) + Arch<D0>::N[i];
+    return o;
+}
+
 template <int K, int N, int MODE>
 MPCD_DEV int ntile_of(int wave, int j)
 {
@@ -156,25 +206,42 @@ MPCD_DEV int ntile_of(int wave, int j)
 
 // One wave-uniform buffer descriptor per layer; chunk (nt, kc, plane) at soffset ((nt*KC+kc)*3+p) KiB.
 template <int K, int N, int MODE>
-MPCD_DEV void load_w3(WFrag3<K, N, MODE> &f, const float *__restrict__ wp, int wave, int lane16)
+MPCD_DEV void load_w3(WLoad<K, N, MODE> &f, const float *__restrict__ wp, int wave, int lane16)
 {
-    using F = WFrag3<K, N, MODE>;
+    using F = WLoad<K, N, MODE>;
     constexpr int KC = F::KC, NT = F::NT;
     const uint64_t a = (uint64_t)wp;
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(3 * K * N * 2), 0x00020000);
+        (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(WPL * K * N * 2), 0x00020000);
+#if MPCD_X3_IDLE_OOB
+    const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0, 0, 0x00020000);
+#endif
 #pragma unroll
     for (int j = 0; j < F::T; ++j) {
         // clamped, not skipped: the load count stays path-independent (a skipped load makes the
         // compiler drain vmcnt(0)); a wave with no tile n uses nothing it loaded
         const int nt = min(ntile_of<K, N, MODE>(wave, j), NT - 1);
+#if MPCD_X3_IDLE_OOB
+        // a wave with no tile n issues its loads against an empty descriptor: out of range, no L2 request
+        const __amdgpu_buffer_rsrc_t rj = ntile_of<K, N, MODE>(wave, j) < NT ? rs : rs0;
+#else
+        const __amdgpu_buffer_rsrc_t rj = rs;
+#endif
+#ifdef MPCD_X3_EXP_NOPL2
+        // timing experiment only (wrong results): the third weight plane read as zeros, no L2 request
+        const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0, 0, 0x00020000);
+#endif
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) {
-                const int soff = __builtin_amdgcn_readfirstlane(((nt * KC + kc) * 3 + pl) * 1024);
-                f.v[j][kc][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
+            for (int pl = 0; pl < WPL; ++pl) {
+                const int soff = __builtin_amdgcn_readfirstlane(((nt * KC + kc) * WPL + pl) * 1024);
+#ifdef MPCD_X3_EXP_NOPL2
+                f.v[j][kc][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(pl == 2 ? rz : rj, lane16, soff, 0));
+#else
+                f.v[j][kc][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rj, lane16, soff, 0));
+#endif
             }
     }
 }
@@ -220,6 +287,7 @@ struct MlpX3 {
     static constexpr int CPW = L::CPW;
     static constexpr int QUADS = D0 / 4;
     using FW = WFrag3<32, D0, PAIRED>;
+    using FWL = WLoad<32, D0, PAIRED>;
     static constexpr int NZT = FW::T;
 
     // Hidden layer l. SPLIT (N = 32): wave w -> column tile (w & 1), n-tiles (w >> 1) + 2j; PAIRED
@@ -426,8 +494,10 @@ struct MlpX3 {
     }
 
     template <int l>
-    static MPCD_DEV void layer(const WFrag3<A::K[l], A::N[l], mode_for<A::N[l], R, W>()> &f, char *lds, int wave, int lane)
+    static MPCD_DEV void layer(const WLoad<A::K[l], A::N[l], mode_for<A::N[l], R, W>()> &wl, char *lds, int wave, int lane)
     {
+        WFrag3<A::K[l], A::N[l], mode_for<A::N[l], R, W>()> f;
+        to_planes(wl, f);
         if constexpr (H8) hidden8<l>(f, lds, wave, lane);
         else hidden<l>(f, lds, wave, lane);
     }
@@ -574,16 +644,16 @@ struct MlpX3 {
         int lane16 = lane * 16;
         const float *wp = p.wpack;
         int wofs = 0;
-        auto wptr = [&](int l) { return wp + wofs + A::woff3(l); };
+        auto wptr = [&](int l) { return wp + wofs + woffx<D0>(l); };
         float *bi = reinterpret_cast<float *>(lds + L::BI);
         float *bic = reinterpret_cast<float *>(lds + L::BIC);
         float *cps = reinterpret_cast<float *>(lds + L::CPS);
 
         for (int l = 0; l < NLAYER; ++l)
-            for (int i = threadIdx.x; i < A::N[l]; i += NTHR) bi[A::boff(l) + i] = wp[A::woff3(l) + 3 * A::K[l] * A::N[l] / 2 + i];
+            for (int i = threadIdx.x; i < A::N[l]; i += NTHR) bi[A::boff(l) + i] = wp[woffx<D0>(l) + wfl<D0>(l) + i];
         for (int j = 0; j < 6; ++j)
             for (int i = threadIdx.x; i < A::N[2 * j + 1]; i += NTHR)
-                bic[cond_off(j) + i] = wp[A::woff3(2 * j + 1) + 3 * A::K[2 * j + 1] * A::N[2 * j + 1] / 2 + i];
+                bic[cond_off(j) + i] = wp[woffx<D0>(2 * j + 1) + wfl<D0>(2 * j + 1) + i];
         for (int i = threadIdx.x; i < COND_TOTAL; i += NTHR) cps[i] = CTX ? p.cproj[i] : 0.f;
         if (threadIdx.x < CPW) reinterpret_cast<uint32_t *>(lds + L::AMX)[threadIdx.x] = 0u;
         uint32_t am[2] = {0u, 0u};
@@ -600,7 +670,7 @@ struct MlpX3 {
             store_x(lds, c, qd * 4, z);
         }
 
-        WFrag3<A::K[0], A::N[0], mode_for<A::N[0], R, W>()> w0;
+        WLoad<A::K[0], A::N[0], mode_for<A::N[0], R, W>()> w0;
         load_w3(w0, wptr(0), wave, lane16);
         f32x4 nz[NZT][NB];
         StepPlan sp = load_plan(p.plan, 0);
@@ -627,7 +697,7 @@ struct MlpX3 {
         for (int s = 0; s < p.n_steps; ++s) {
             // launder the weight base: stops LICM hoisting every layer's weight loads out of the loop
             asm volatile("" : "+s"(wofs), "+v"(lane16));
-            WFrag3<A::K[1], A::N[1], mode_for<A::N[1], R, W>()> w1;
+            WLoad<A::K[1], A::N[1], mode_for<A::N[1], R, W>()> w1;
             load_w3(w1, wptr(1), wave, lane16);
             bar(0);
             // this step's time projections + cond biases (+ shared context part) -> TPU / TPC
@@ -638,27 +708,27 @@ struct MlpX3 {
             }
             tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 1 < p.n_steps ? s + 1 : s) * COND_TOTAL)[tpi];
             layer<0>(w0, lds, wave, lane);
-            WFrag3<A::K[2], A::N[2], mode_for<A::N[2], R, W>()> w2;
+            WLoad<A::K[2], A::N[2], mode_for<A::N[2], R, W>()> w2;
             load_w3(w2, wptr(2), wave, lane16);
             bar(1);
             layer<1>(w1, lds, wave, lane);
-            WFrag3<A::K[3], A::N[3], mode_for<A::N[3], R, W>()> w3;
+            WLoad<A::K[3], A::N[3], mode_for<A::N[3], R, W>()> w3;
             load_w3(w3, wptr(3), wave, lane16);
             bar(2);
             layer<2>(w2, lds, wave, lane);
-            WFrag3<A::K[4], A::N[4], mode_for<A::N[4], R, W>()> w4;
+            WLoad<A::K[4], A::N[4], mode_for<A::N[4], R, W>()> w4;
             load_w3(w4, wptr(4), wave, lane16);
             bar(3);
             layer<3>(w3, lds, wave, lane);
-            WFrag3<A::K[5], A::N[5], mode_for<A::N[5], R, W>()> w5;
+            WLoad<A::K[5], A::N[5], mode_for<A::N[5], R, W>()> w5;
             load_w3(w5, wptr(5), wave, lane16);
-            WFrag3<A::K[6], A::N[6], mode_for<A::N[6], R, W>()> w6;
+            WLoad<A::K[6], A::N[6], mode_for<A::N[6], R, W>()> w6;
 #if MPCD_X3_LEAD2  // the 128-wide layers' weights two segments ahead (their L2 latency outlasts one segment)
             load_w3(w6, wptr(6), wave, lane16);
 #endif
             bar(4);
             layer<4>(w4, lds, wave, lane);
-            WFrag3<A::K[7], A::N[7], mode_for<A::N[7], R, W>()> w7;
+            WLoad<A::K[7], A::N[7], mode_for<A::N[7], R, W>()> w7;
 #if MPCD_X3_LEAD2
             load_w3(w7, wptr(7), wave, lane16);
 #else
@@ -671,27 +741,27 @@ struct MlpX3 {
 #endif
             bar(6);
             layer<6>(w6, lds, wave, lane);
-            WFrag3<A::K[8], A::N[8], mode_for<A::N[8], R, W>()> w8;
+            WLoad<A::K[8], A::N[8], mode_for<A::N[8], R, W>()> w8;
             load_w3(w8, wptr(8), wave, lane16);
             bar(7);
             layer<7>(w7, lds, wave, lane);
-            WFrag3<A::K[9], A::N[9], mode_for<A::N[9], R, W>()> w9;
+            WLoad<A::K[9], A::N[9], mode_for<A::N[9], R, W>()> w9;
             load_w3(w9, wptr(9), wave, lane16);
             bar(8);
             layer<8>(w8, lds, wave, lane);
-            WFrag3<A::K[10], A::N[10], mode_for<A::N[10], R, W>()> w10;
+            WLoad<A::K[10], A::N[10], mode_for<A::N[10], R, W>()> w10;
             load_w3(w10, wptr(10), wave, lane16);
             bar(9);
             layer<9>(w9, lds, wave, lane);
-            WFrag3<A::K[11], A::N[11], mode_for<A::N[11], R, W>()> w11;
+            WLoad<A::K[11], A::N[11], mode_for<A::N[11], R, W>()> w11;
             load_w3(w11, wptr(11), wave, lane16);
             bar(10);
             layer<10>(w10, lds, wave, lane);
-            WFrag3<A::K[12], A::N[12], mode_for<A::N[12], R, W>()> w12;
+            WLoad<A::K[12], A::N[12], mode_for<A::N[12], R, W>()> w12;
             load_w3(w12, wptr(12), wave, lane16);
             bar(11);
             layer<11>(w11, lds, wave, lane);
-            FW w13;
+            FWL w13;
             load_w3(w13, wptr(13), wave, lane16);
             bar(12);
             layer<12>(w12, lds, wave, lane);
@@ -708,7 +778,11 @@ struct MlpX3 {
             // next step's layer-0 weights; unconditional (a path-dependent load count drains vmcnt(0))
             load_w3(w0, wptr(0), wave, lane16);
             bar(13);
-            if (wave < 4) final_and_update(w13, lds, p, cur, s, cand0, nzc, am, wave, lane);
+            if (wave < 4) {
+                FW f13;
+                to_planes(w13, f13);
+                final_and_update(f13, lds, p, cur, s, cand0, nzc, am, wave, lane);
+            }
         }
         if (SMODE != MODE_EPS && SMODE != MODE_EPS1 && p.chain_absmax) {
             const int col = lane & 15;
@@ -809,9 +883,9 @@ void mlp_x3_force_layout(int layout) { g_force_layout.store(layout); }
 int mlp_packed_floats_x3(int d0)
 {
     switch (d0) {
-    case 32: return Arch<32>::total3();
-    case 64: return Arch<64>::total3();
-    case 128: return Arch<128>::total3();
+    case 32: return woffx<32>(NLAYER);
+    case 64: return woffx<64>(NLAYER);
+    case 128: return woffx<128>(NLAYER);
     default: return -1;
     }
 }
@@ -849,6 +923,10 @@ void mlp_pack_weights_x3(int d0, const float *const *lin_w, const float *const *
                 for (int lane = 0; lane < 64; ++lane)
                     for (int j = 0; j < 8; ++j) {
                         const float w = lin_w[l][(size_t)(nt * 16 + (lane & 15)) * K + kc * 32 + 8 * (lane >> 4) + j];
+                        if (WPL == 2) {  // fp32 as loaded; the kernel splits it (to_planes)
+                            out[o + ((size_t)(nt * KC + kc) * 64 + lane) * 8 + j] = w;
+                            continue;
+                        }
                         const uint16_t h0 = bf16_rne(w);
                         const float r1 = w - bf16_val(h0);
                         const uint16_t h1 = bf16_rne(r1);
@@ -858,7 +936,7 @@ void mlp_pack_weights_x3(int d0, const float *const *lin_w, const float *const *
                         for (int pl = 0; pl < 3; ++pl)
                             pk[(((size_t)(nt * KC + kc) * 3 + pl) * 64 + lane) * 8 + j] = hs[pl];
                     }
-        o += (size_t)3 * K * N / 2;
+        o += (size_t)WPL * K * N / 2;
         for (int n = 0; n < N; ++n) out[o + n] = lin_b[l][n];
         o += N;
     }

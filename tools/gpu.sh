@@ -11,6 +11,8 @@
 #   upmc[:<cfg>]        U-Net per-launch roofline passes over tools/unet_perf.py (trace + FETCH_SIZE +
 #                       WRITE_SIZE + MFMA busy), tune cache shared       -> gpurun_out/uroof/<cfg>_*
 #   unet[:<cfg>]        tools/unet_perf.py timing of one sample call      -> gpurun_out/unet_<cfg>.log
+#   mlpab:<variant>     cfg2 bench with libmpcd_<variant>.so (experiment build) -> gpurun_out/mlpab_<variant>.log
+#   l2pmc[:<workload>]  L1->L2 read requests and L2 hit / miss counters of that bench -> gpurun_out/prof/l2pmc_*
 #
 # Extra bench.py arguments for bench / trace / pmc come from $BENCH_ARGS; extra pytest arguments from
 # $PYTEST_ARGS; extra unet_perf.py arguments from $UNET_ARGS.
@@ -51,6 +53,19 @@ run_job() {
         timeout -s KILL 300 rocprofv3 --pmc $c -d "gpurun_out/prof/pmc_${w}_$c" -o run -f csv -- \
           python3 bench.py --workload "$w" --no-cpu-baseline --steps 3 --warmup 1 $BENCH_ARGS \
           > "gpurun_out/prof/pmc_${w}_$c.log" 2>&1 || return $?
+      done ;;
+    mlpab)
+      # cfg2 bench line of an experiment build (python -m mpc_via_diffusion_model_amd.build <variant> DEF=..)
+      MPCD_LIB=$PWD/mpc_via_diffusion_model_amd/libmpcd_$arg.so timeout -k 10 300 python -u bench.py --workload cfg2 \
+        --no-cpu-baseline $BENCH_ARGS > "gpurun_out/mlpab_$arg.log" 2>&1 ;;
+    l2pmc)
+      # cache counters of the cfg2 bench (one block per pass): L1 -> L2 read requests, L2 hits / misses
+      local w=${arg:-cfg2} c i=0
+      for c in "TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum" "TCC_HIT_sum TCC_MISS_sum"; do
+        timeout -s KILL 120 rocprofv3 --pmc $c -d "gpurun_out/prof/l2pmc_${w}_$i" -o run -f csv -- \
+          python3 bench.py --workload "$w" --no-cpu-baseline --no-shard-probe --steps 3 --warmup 1 $BENCH_ARGS \
+          > "gpurun_out/prof/l2pmc_${w}_$i.log" 2>&1 || return $?
+        i=$((i + 1))
       done ;;
     unet)
       local c=${arg:-cfg5}
