@@ -59,11 +59,18 @@ constexpr int ROWS_MAX = 32;
 #ifndef MPCD_X3_ILV
 #define MPCD_X3_ILV 1
 #endif
+// Experiment switches, all off in the product build (profiles/r3_mlp_vmem_ab.txt: every one measured slower):
+// MPCD_X3_WF32 fp32 weight stream split in registers (unfinished: also fails the cfg1 headline parity test),
+// MPCD_X3_SKIP_IDLE 1/2 idle waves issue no weight loads (branch / lane mask), MPCD_X3_EXP_NOPL2 timing probe
+// with the third weight plane's loads not issued (wrong results).
 #ifndef MPCD_X3_WF32
 #define MPCD_X3_WF32 0
 #endif
-#ifndef MPCD_X3_IDLE_OOB
-#define MPCD_X3_IDLE_OOB 0
+#ifndef MPCD_X3_SKIP_IDLE
+#define MPCD_X3_SKIP_IDLE 0
+#endif
+#ifndef MPCD_X3_EXP_NOPL2
+#define MPCD_X3_EXP_NOPL2 0
 #endif
 constexpr int THREADS = 64 * MPCD_X3_WAVES;
 constexpr int WAVES = THREADS / 64;
@@ -206,7 +213,7 @@ MPCD_DEV int ntile_of(int wave, int j)
 
 // One wave-uniform buffer descriptor per layer; chunk (nt, kc, plane) at soffset ((nt*KC+kc)*3+p) KiB.
 template <int K, int N, int MODE>
-MPCD_DEV void load_w3(WLoad<K, N, MODE> &f, const float *__restrict__ wp, int wave, int lane16)
+MPCD_DEV void load_w3(WLoad<K, N, MODE> &f, const float *__restrict__ wp, int wave, int lane16, bool need = true)
 {
     using F = WLoad<K, N, MODE>;
     constexpr int KC = F::KC, NT = F::NT;
@@ -214,33 +221,49 @@ MPCD_DEV void load_w3(WLoad<K, N, MODE> &f, const float *__restrict__ wp, int wa
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(WPL * K * N * 2), 0x00020000);
-#if MPCD_X3_IDLE_OOB
-    const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0, 0, 0x00020000);
-#endif
 #pragma unroll
     for (int j = 0; j < F::T; ++j) {
-        // clamped, not skipped: the load count stays path-independent (a skipped load makes the
-        // compiler drain vmcnt(0)); a wave with no tile n uses nothing it loaded
         const int nt = min(ntile_of<K, N, MODE>(wave, j), NT - 1);
-#if MPCD_X3_IDLE_OOB
-        // a wave with no tile n issues its loads against an empty descriptor: out of range, no L2 request
-        const __amdgpu_buffer_rsrc_t rj = ntile_of<K, N, MODE>(wave, j) < NT ? rs : rs0;
+#if MPCD_X3_SKIP_IDLE == 2
+        // A wave with no tile n (or need = false) runs its loads with every lane masked off: the
+        // instructions stay on every path (no control flow, so no vmcnt drain at a join) but move no data
+        const int lim = (need && ntile_of<K, N, MODE>(wave, j) < NT) ? 64 * 16 : 0;
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+            for (int pl = 0; pl < WPL; ++pl) {
+                const int soff = __builtin_amdgcn_readfirstlane(((nt * KC + kc) * WPL + pl) * 1024);
+                u32x4 v = u32x4{0u, 0u, 0u, 0u};
+                if (lane16 < lim) v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
+                f.v[j][kc][pl] = v;
+            }
+        continue;
+#elif MPCD_X3_SKIP_IDLE
+        // A wave with no tile n (or that does not run the layer: need = false) issues no loads. The
+        // vector-memory pipe, not the L2, is what the weight stream saturates: every 16-byte-per-lane
+        // load costs a CU the same issue time whether or not its data is used (profiles/r3_mlp_vmem_ab.txt).
+        if (!need || ntile_of<K, N, MODE>(wave, j) >= NT) {
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+                for (int pl = 0; pl < WPL; ++pl) f.v[j][kc][pl] = u32x4{0u, 0u, 0u, 0u};
+            continue;
+        }
 #else
-        const __amdgpu_buffer_rsrc_t rj = rs;
-#endif
-#ifdef MPCD_X3_EXP_NOPL2
-        // timing experiment only (wrong results): the third weight plane read as zeros, no L2 request
-        const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0, 0, 0x00020000);
+        // clamped, not skipped: the load count stays path-independent; a wave with no tile n uses
+        // nothing it loaded
+        (void)need;
 #endif
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
             for (int pl = 0; pl < WPL; ++pl) {
                 const int soff = __builtin_amdgcn_readfirstlane(((nt * KC + kc) * WPL + pl) * 1024);
-#ifdef MPCD_X3_EXP_NOPL2
-                f.v[j][kc][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(pl == 2 ? rz : rj, lane16, soff, 0));
+#if MPCD_X3_EXP_NOPL2
+                // timing experiment only (wrong results): the third plane's load not issued
+                f.v[j][kc][pl] = pl == 2 ? u32x4{0u, 0u, 0u, 0u} : __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
 #else
-                f.v[j][kc][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rj, lane16, soff, 0));
+                f.v[j][kc][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
 #endif
             }
     }
@@ -762,7 +785,7 @@ struct MlpX3 {
             bar(11);
             layer<11>(w11, lds, wave, lane);
             FWL w13;
-            load_w3(w13, wptr(13), wave, lane16);
+            load_w3(w13, wptr(13), wave, lane16, wave < 4);
             bar(12);
             layer<12>(w12, lds, wave, lane);
             const StepPlan cur = sp;
