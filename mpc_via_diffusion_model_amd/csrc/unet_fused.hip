@@ -66,6 +66,11 @@ struct COp {
     int spill;             // also write the output to the skip scratch (RESTORE: read it back)
     CView in, res, out;
 };
+// MPCD_FUSED_GN1 = 1: GroupNorm statistics in one pass (sums and sums of squares reduced together,
+// var = E[x^2] - mean^2) instead of the exact two-pass; experiment switch
+#ifndef MPCD_FUSED_GN1
+#define MPCD_FUSED_GN1 0
+#endif
 constexpr int kMaxOps = 40;
 struct Prog {
     COp ops[kMaxOps];
@@ -616,6 +621,40 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
         const bool leader = col == 0 && (q & QMASK) == 0;
         int slot[NTW];
         float m[NTW];
+#if MPCD_FUSED_GN1
+        // one pass, one barrier: both partial sums of each half row through LDS together
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+            slot[j] = (row * kGroups + (n0[j] >> op.cpg_sh)) * 2;
+            f32x2 p1 = lo2(acc[j][0]) + hi2(acc[j][0]);
+            f32x2 p2 = fma2(hi2(acc[j][0]), hi2(acc[j][0]), lo2(acc[j][0]) * lo2(acc[j][0]));
+#pragma unroll
+            for (int cc = 1; cc < NCW; ++cc) {
+                const f32x2 a0 = lo2(acc[j][cc]), a1 = hi2(acc[j][cc]);
+                p1 += a0 + a1;
+                p2 = fma2(a1, a1, fma2(a0, a0, p2));
+            }
+            float ss[2] = {p1[0] + p1[1], p2[0] + p2[1]};
+            group_sum_n<16, QMASK, 2>(ss);
+            if (leader) {
+                st[slot[j] + half] = ss[0];
+                st[2 * R * kGroups + slot[j] + half] = ss[1];
+            }
+        }
+        lds_barrier();
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+            const f32x2 w1 = *reinterpret_cast<const f32x2 *>(st + slot[j]);
+            const f32x2 w2 = *reinterpret_cast<const f32x2 *>(st + 2 * R * kGroups + slot[j]);
+            m[j] = (w1.x + w1.y) * inv_n;
+            const float rs = rsqrt_nr(fmaxf((w2.x + w2.y) * inv_n - m[j] * m[j], 0.f) + 1e-5f);
+#pragma unroll
+            for (int cc = 0; cc < NCW; ++cc) {
+                mean[j][cc] = m[j];
+                rstd[j][cc] = rs;
+            }
+        }
+#else
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
             slot[j] = (row * kGroups + (n0[j] >> op.cpg_sh)) * 2;
@@ -651,11 +690,46 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
                 rstd[j][cc] = rs;
             }
         }
+#endif
     } else if constexpr (GN) {  // every (row, group) inside the wave
         constexpr int L = op.lout, SEG = L < 16 ? L : 16, TPR = L > 16 ? L / 16 : 1;  // column tiles per row
         constexpr float inv_n = 1.0f / (float)(L << op.cpg_sh);
         static_assert(NCW % TPR == 0, "a wave's column tiles are whole rows");
         constexpr int NR = NCW / TPR, NS = NTW * NR;  // (n-tile, row) sums of the wave, reduced side by side
+#if MPCD_FUSED_GN1
+        // one pass: the sums and the sums of squares reduced side by side (one DPP chain's latency),
+        // var = E[x^2] - mean^2 (clamped at 0)
+        float ss[2 * NS];
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                f32x2 p1 = lo2(acc[j][r * TPR]) + hi2(acc[j][r * TPR]);
+                f32x2 p2 = fma2(hi2(acc[j][r * TPR]), hi2(acc[j][r * TPR]), lo2(acc[j][r * TPR]) * lo2(acc[j][r * TPR]));
+#pragma unroll
+                for (int t = 1; t < TPR; ++t) {
+                    const f32x2 a0 = lo2(acc[j][r * TPR + t]), a1 = hi2(acc[j][r * TPR + t]);
+                    p1 += a0 + a1;
+                    p2 = fma2(a1, a1, fma2(a0, a0, p2));
+                }
+                ss[j * NR + r] = p1[0] + p1[1];
+                ss[NS + j * NR + r] = p2[0] + p2[1];
+            }
+        group_sum_n<SEG, QMASK, 2 * NS>(ss);
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const float m = ss[j * NR + r] * inv_n;
+                const float var = fmaxf(ss[NS + j * NR + r] * inv_n - m * m, 0.f);
+                const float rs = rsqrt_nr(var + 1e-5f);
+#pragma unroll
+                for (int t = 0; t < TPR; ++t) {
+                    mean[j][r * TPR + t] = m;
+                    rstd[j][r * TPR + t] = rs;
+                }
+            }
+#else
         float s1[NS], s2[NS];
 #pragma unroll
         for (int j = 0; j < NTW; ++j)
@@ -693,6 +767,7 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
                     rstd[j][r * TPR + t] = rs;
                 }
             }
+#endif
     } else if constexpr (op.alias_in) {
         lds_barrier();
     }
