@@ -80,5 +80,6 @@ struct RolloutSelect {
     unsigned *counter;    // zero-initialised, reset by the kernel
     int64_t n_part;       // capacity of part_* (>= ceil(batch / 64))
     int64_t offset;
+    int32_t *code_out;    // optional: the clip code flags[0], written with the winner (mpcd_mpc_step's result block)
 };
 constexpr int kRolloutBlock = 64;  // candidates per rollout workgroup

@@ -1096,8 +1096,9 @@ int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, fl
     float *u_dev = reinterpret_cast<float *>(best_dev + 1);
     double *part_cost = c->step_part.as<double>();
     int64_t *part_idx = reinterpret_cast<int64_t *>(part_cost + n_part);
-    if (!c->comm) {  // rollout + cost + argmin + the winner's unnormalised row in one launch
-        RolloutSelect sel{best_dev, u_dev, part_cost, part_idx, c->sync_ws() + 8, n_part, sa.global_offset};
+    int32_t *code_dev = reinterpret_cast<int32_t *>(u_dev + row);
+    if (!c->comm) {  // rollout + cost + argmin + the winner's unnormalised row + the clip code in one launch
+        RolloutSelect sel{best_dev, u_dev, part_cost, part_idx, c->sync_ws() + 8, n_part, sa.global_offset, code_dev};
         HIP_TRY(launch_rollout_cost(sys, a->x0, nullptr, B, sa.x_out, a->act_min, a->act_max, flag, B, H,
                                     a->cost_local, st, &sel));
     } else {
@@ -1109,9 +1110,8 @@ int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, fl
         HIP_TRY(launch_winner_row(best_dev, (int64_t)c->rank * B, B, sa.x_out, row, row_norm, st));
         if ((rc = comm_reduce(c, row_norm, (size_t)row, COMM_SUM_F32, st))) return rc;
         HIP_TRY(launch_unnormalize(row_norm, row, d.state_dim, flag, a->act_min, a->act_max, u_dev, st));
+        HIP_TRY(hipMemcpyAsync(code_dev, flag, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     }
-    int32_t *code_dev = reinterpret_cast<int32_t *>(u_dev + row);
-    HIP_TRY(hipMemcpyAsync(code_dev, flag, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     void *host_out = static_cast<char *>(c->step_host) + 64;
     HIP_TRY(hipMemcpyAsync(host_out, c->step_out.p, out_bytes, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));

@@ -41,6 +41,7 @@ struct SelectK {
     int64_t *part_idx;   // [gridDim.x]
     unsigned *counter;
     int64_t offset;      // global index of candidate 0
+    int32_t *code_out;   // optional: flags[0] copied next to the winner (saves the caller a device copy)
 };
 
 // (v, i) beats (bv, bi): NaN = +inf, lower cost, then lower index; i < 0 = empty
@@ -303,6 +304,7 @@ __global__ __launch_bounds__(RT_THREADS) void rollout_cost_kernel(const SysK S, 
             K.best->cost = v;
             K.best->index = i < 0 ? -1 : K.offset + i;
             *K.counter = 0u;
+            if (K.code_out) *K.code_out = flags[0];
         }
         if (i >= 0 && K.row_out) {
             const bool clip0 = flags[0] == 1;
@@ -507,7 +509,7 @@ hipError_t launch_rollout_cost(const mpcd_system_desc &d, const double *x0_host,
     SelectK K = {};
     if (sel) {
         if (group != batch || sel->n_part < (batch + RT_THREADS - 1) / RT_THREADS) return hipErrorInvalidValue;
-        K = SelectK{sel->best, sel->row_out, sel->part_cost, sel->part_idx, sel->counter, sel->offset};
+        K = SelectK{sel->best, sel->row_out, sel->part_cost, sel->part_idx, sel->counter, sel->offset, sel->code_out};
     }
     const dim3 grid((unsigned)((batch + RT_THREADS - 1) / RT_THREADS));
 #define MPCD_ROLLOUT(SYS_)                                                                                          \
