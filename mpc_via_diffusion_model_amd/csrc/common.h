@@ -30,6 +30,18 @@ MPCD_DEV float mish(float x)
     return x * __builtin_fmaf(-2.0f, r, 1.0f);
 }
 
+// mish() for the SLP-vectorizable epilogues (csrc/mlp_x3.hip, mlp_sampler.hip, unet_mx.hip): the empty register
+// fence on the result keeps each element's Mish in scalar VALU ops. Packed by hipcc's SLP vectorizer (ROCm 7.2)
+// such epilogues read v_rcp_f32 results with a v_pk_fma_f32 one wait state later, and a build with that pattern
+// gave wrong conv outputs on the GPU (profiles/r3_hazard_ab.txt); tests/test_isa.py keeps every kernel of
+// libmpcd.so free of it. The fused U-Net packs its Mish by hand with >= 2 wait states and does not use this.
+MPCD_DEV float mish_scalar(float x)
+{
+    float y = mish(x);
+    asm volatile("" : "+v"(y));
+    return y;
+}
+
 // torch.clamp(x, -1, 1) / torch.clip: a NaN stays NaN (fminf / fmaxf alone would return the bound), so a
 // non-finite noise prediction propagates to the samples as in the reference instead of turning into -1.
 MPCD_DEV float clamp1(float x)
@@ -72,12 +84,11 @@ MPCD_DEV f32x4 philox_normal4(uint64_t seed, uint64_t cand, uint32_t step, uint3
     const float u2 = ((float)r.z + 1.0f) * s, u3 = (float)r.w * s;
     const float ra = __fsqrt_rn(-2.0f * __logf(u0)), rb = __fsqrt_rn(-2.0f * __logf(u2));
     const float ta = 6.2831853071795865f * u1, tb = 6.2831853071795865f * u3;
-    f32x4 z;
-    z.x = ra * __cosf(ta);
-    z.y = ra * __sinf(ta);
-    z.z = rb * __cosf(tb);
-    z.w = rb * __sinf(tb);
-    return z;
+    // each product in a scalar op (the fence stops SLP packing ra * {cos, sin} into a v_pk_mul_f32 one wait
+    // state behind v_sin_f32: the pattern tests/test_isa.py forbids, see mish_scalar)
+    float z0 = ra * __cosf(ta), z1 = ra * __sinf(ta), z2 = rb * __cosf(tb), z3 = rb * __sinf(tb);
+    asm volatile("" : "+v"(z0), "+v"(z1), "+v"(z2), "+v"(z3));
+    return f32x4{z0, z1, z2, z3};
 }
 
 // One denoise step of the plan (built on the host from the schedule buffers).

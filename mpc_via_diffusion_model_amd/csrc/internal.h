@@ -70,6 +70,8 @@ int mlp_packed_floats_x3(int d0);
 void mlp_x3_force_layout(int layout);  // mpcd_mlp_force_layout
 void mlp_pack_weights_x3(int d0, const float *const *lin_w, const float *const *lin_b, float *out);
 hipError_t launch_mlp_x3(int d0, int nb, const MlpSampleArgs &a, hipStream_t stream);
+// resident-weight variant (mlp_rw.hip), selected by mlp_x3's layout choice: rows = 32 or 16 per workgroup
+hipError_t launch_mlp_rw(int d0, int rows, const MlpSampleArgs &a, hipStream_t stream);
 
 // Fused selection for launch_rollout_cost (single rank): see rollout.hip SelectK
 struct RolloutSelect {

@@ -1,0 +1,547 @@
+// Persistent CFG-DDPM / DDIM sampler for the MLP noise-net, fp32-accurate split-bf16
+// GEMMs, with the three 128x128 layers' weights RESIDENT in registers for the whole launch.
+//
+// Why (profiles/r3_mlp_vmem_ab.txt): the streaming kernel (mlp_x3.hip) re-reads every
+// layer's three-plane weights from L2 each denoise step, 888 KB per CU per step, and that per-CU
+// vector-memory stream - not L2 bandwidth, not MFMA - sets its step time. A CU's register file is
+// 512 KiB (4 SIMDs x 512 registers x 64 lanes x 4 B): with one wave per SIMD (4 waves, 512 registers
+// each) the 288 KiB of Linear 5/6/7 (K = N = 128; wave w owns n-tiles w and w + 4: 24 fragments of
+// 16 B per lane per layer) stay in registers across all denoise steps - 63 fragments in AGPRs, read
+// directly as the MFMA A operand, 9 in VGPRs. Every other layer streams once per CU per step (each
+// fragment loaded by the one wave that uses it, except the N = 32 layers at 32 rows, split by column
+// tile: 324 KB per CU per step instead of 888).
+//
+// Same pack, LDS layout, layer order, MFMA order (six partial products of each 32-k chunk, smallest
+// first, k-chunks in order, accumulators initialised from the bias / cond tables), Mish, split and
+// denoise update as mlp_x3_kernel, so its results are bit-identical to the streaming kernel's
+// (tests/test_gpu_mlp.py checks it).
+#include <hip/hip_runtime.h>
+
+#include "mlp_x3.h"
+
+namespace {
+using namespace mlpx3;
+static_assert(WPL == 3, "mlp_rw streams the three-plane pack");
+
+constexpr int RW_W = 4;           // waves per workgroup (one per SIMD, 512 registers each)
+constexpr int RW_T = 64 * RW_W;   // threads
+constexpr int RES_L0 = 5;         // resident layers 5, 6, 7
+constexpr int RES_NL = 3;
+constexpr int RES_G = RES_NL * 2 * 4;  // groups (layer, n-tile j, k-chunk) of 3 plane fragments per wave: 24
+constexpr int RES_AG = 21;             // groups 0..20 resident in AGPRs (63 fragments, 252 registers); the
+                                       // last three (layer 7, n-tile w + 4, k-chunks 1-3) stream each step
+
+// Six partial products of one 32-k chunk with the weight planes in AGPRs (the A operand of an MFMA may be
+// an AGPR on gfx950; hipcc does not allocate builtin operands there, so the chain is written out). One
+// statement of six dependent MFMAs: back-to-back srcC forwarding of the same opcode needs no wait states
+// (hipcc emits none between the builtin form of this chain). The leading s_nop covers a VALU write of
+// acc right before the statement (the 2-wait-state VALU-write -> MFMA-read rule, which the compiler's
+// hazard pass does not apply to inline asm); the MFMA result -> VALU read wait after the statement is
+// inserted by the compiler (checked in tests/test_isa.py).
+MPCD_DEV f32x4 mfma_x3_agpr(const u32x4 &w0, const u32x4 &w1, const u32x4 &w2, const u32x4 (&x)[3], f32x4 acc)
+{
+    asm("s_nop 1\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %3, %4, %0\n\t"   // w2 x0
+        "v_mfma_f32_16x16x32_bf16 %0, %2, %5, %0\n\t"   // w1 x1
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %6, %0\n\t"   // w0 x2
+        "v_mfma_f32_16x16x32_bf16 %0, %2, %4, %0\n\t"   // w1 x0
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %5, %0\n\t"   // w0 x1
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0"       // w0 x0
+        : "+v"(acc)
+        : "a"(w0), "a"(w1), "a"(w2), "v"(x[0]), "v"(x[1]), "v"(x[2]));
+    return acc;
+}
+
+template <int D0, int SMODE, bool CTX, int R>
+struct MlpRw {
+    static constexpr int NB = (SMODE == MODE_DDIM || SMODE == MODE_EPS1) ? 1 : 2;
+    static constexpr bool IS_DDPM = SMODE == MODE_DDPM_CFG || SMODE == MODE_DDPM_XN;
+    static_assert(R == 32 || R == 16, "32 or 16 rows per workgroup");
+    static constexpr int NCT = R / 16;  // 16-row column tiles
+    using A = Arch<D0>;
+    using L = Lds3<D0, NB, R>;
+    static constexpr int CPW = L::CPW;
+    static constexpr int QUADS = D0 / 4;
+
+    // R = 16 with CFG: columns 0-7 are the context rows of candidates 0-7, 8-15 their masked rows
+    static MPCD_DEV int cand_of(int ct, int col) { return NB == 2 ? (R == 16 ? (col & 7) : col) : ct * 16 + col; }
+    static MPCD_DEV bool masked_of(int ct, int col) { return NB == 2 && (R == 16 ? col >= 8 : ct == 1); }
+
+    // Layer l's work per wave. N = 32 at 32 rows (SPL): wave w -> n-tile w & 1, column tile w >> 1. Otherwise
+    // wave w -> n-tiles w + 4j (j < T) for every column tile; a wave with no tile (N = 32 at 16 rows) loads
+    // a clamped copy and computes nothing.
+    template <int l> static constexpr bool SPL = A::N[l] == 32 && NCT == 2;
+    template <int l> static constexpr int TL = SPL<l> ? 1 : (A::N[l] / 16 + 3) / 4;
+    template <int l> static constexpr int CL = SPL<l> ? 1 : NCT;
+    template <int l> static MPCD_DEV int nt_of(int wave, int j) { return SPL<l> ? (wave & 1) : wave + 4 * j; }
+    template <int l> static MPCD_DEV int ct_of(int wave, int c) { return SPL<l> ? (wave >> 1) : c; }
+
+    // streamed fragments of layer l for this wave
+    template <int l>
+    struct WS {
+        u32x4 v[TL<l>][A::K[l] / 32][3];
+    };
+
+    template <int l>
+    static MPCD_DEV void load_ws(WS<l> &f, const float *__restrict__ wp, int wave, int lane16)
+    {
+        constexpr int K = A::K[l], N = A::N[l], KC = K / 32, NT = N / 16;
+        const uint64_t a = (uint64_t)(wp + woffx<D0>(l));
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(3 * K * N * 2), 0x00020000);
+#pragma unroll
+        for (int j = 0; j < TL<l>; ++j) {
+            const int nt = min(nt_of<l>(wave, j), NT - 1);  // clamped: path-independent load count
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) {
+                    const int soff = __builtin_amdgcn_readfirstlane(((nt * KC + kc) * 3 + pl) * 1024);
+                    f.v[j][kc][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
+                }
+        }
+    }
+
+    // Resident fragments: group g = ((li * 2 + j) * 4 + kc), planes 0..2 (AGPRs); Tail: groups RES_AG.. of
+    // layer 7, streamed like the other layers (VGPRs)
+    struct Res {
+        u32x4 a[RES_AG][3];
+    };
+    struct Tail {
+        u32x4 v[RES_G - RES_AG][3];
+    };
+    static MPCD_DEV void load_tail(Tail &t, const float *__restrict__ wp, int wave, int lane16)
+    {
+        const uint64_t a = (uint64_t)(wp + woffx<D0>(RES_L0 + RES_NL - 1));
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(3 * 128 * 128 * 2), 0x00020000);
+#pragma unroll
+        for (int g = RES_AG; g < RES_G; ++g) {
+            const int j = (g / 4) & 1, kc = g & 3, nt = wave + 4 * j;
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                const int soff = __builtin_amdgcn_readfirstlane(((nt * 4 + kc) * 3 + pl) * 1024);
+                t.v[g - RES_AG][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
+            }
+        }
+    }
+
+    static MPCD_DEV void load_res(Res &r, const float *__restrict__ wp, int wave, int lane)
+    {
+#pragma unroll
+        for (int g = 0; g < RES_AG; ++g) {
+            const int li = g / 8, j = (g / 4) & 1, kc = g & 3;
+            const int nt = wave + 4 * j;
+            const float *base = wp + woffx<D0>(RES_L0 + li) + (size_t)((nt * 4 + kc) * 3) * 256 + lane * 4;
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                r.a[g][pl] = __builtin_bit_cast(u32x4, ldg4(base + pl * 256));
+            }
+        }
+    }
+
+    // Hidden layer l: per n-tile pass j, k-chunks in order over this wave's column tiles; pass j's epilogue
+    // (Mish, 3-way split, LDS stores of the next layer's operand planes) is issued behind pass j + 1's MFMAs.
+    // MM(j, kc, x[3], acc) -> acc: the six partial products with this wave's fragments of (j, kc).
+    template <int l, class MM>
+    static MPCD_DEV void hidden(MM mm, char *lds, int wave, int lane)
+    {
+        constexpr int K = A::K[l], N = A::N[l], KC = K / 32, NT = N / 16, T = TL<l>, NC = CL<l>, EPI = epi_of(l);
+        const int col = lane & 15, q = lane >> 4;
+        constexpr bool in_shared = l == 0 && NB == 2;  // CFG: both branches read the candidate's x
+        static_assert(T == 1 || NT % 4 == 0, "only a one-tile layer can leave a wave idle");
+        if constexpr (NT < 4 && !SPL<l>)
+            if (wave >= NT) return;  // N = 32 at 16 rows: waves 2, 3 have no tile
+        f32x4 acc[T][NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int ct = ct_of<l>(wave, c);
+            const float *init = reinterpret_cast<const float *>(
+                lds + (EPI == EPI_CMISH ? (masked_of(ct, col) ? L::TPU : L::TPC) + cond_off(l / 2) * 4
+                                        : L::BI + A::boff(l) * 4));
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+                acc[j][c] = *reinterpret_cast<const f32x4 *>(init + min(nt_of<l>(wave, j), NT - 1) * 16 + 4 * q);
+        }
+        auto ldx = [&](u32x4 (&x)[NC][3], int kc) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int ct = ct_of<l>(wave, c);
+                const int row = in_shared ? cand_of(ct, col) : ct * 16 + col;
+                load_x3(x[c], lds + L::in_off(l) + row * L::in_rs(l) + (kc * 32 + 8 * q) * 2, L::in_pl(l));
+            }
+        };
+        auto epi = [&](int j, int c) {
+            const int n = nt_of<l>(wave, j) * 16 + 4 * q;
+            f32x4 v = acc[j][c];
+            if (EPI != EPI_NONE) {
+                v.x = mish_scalar(v.x);
+                v.y = mish_scalar(v.y);
+                v.z = mish_scalar(v.z);
+                v.w = mish_scalar(v.w);
+            }
+            u32x2 p0, p1, p2;
+            split3(v, p0, p1, p2);
+            char *o = lds + L::out_off(l) + (ct_of<l>(wave, c) * 16 + col) * L::out_rs(l) + n * 2;
+            *reinterpret_cast<u32x2 *>(o) = p0;
+            *reinterpret_cast<u32x2 *>(o + L::out_pl(l)) = p1;
+            *reinterpret_cast<u32x2 *>(o + 2 * L::out_pl(l)) = p2;
+        };
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            u32x4 xc[NC][3], xn[NC][3];
+            ldx(xc, 0);
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc) {
+                if (kc + 1 < KC) ldx(xn, kc + 1);
+#pragma unroll
+                for (int c = 0; c < NC; ++c) acc[j][c] = mm(j, kc, xc[c], acc[j][c]);
+                if (j > 0 && kc == 0) {
+                    // the previous pass's epilogue in this pass's MFMA shadow
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) epi(j - 1, c);
+                }
+                if (kc + 1 < KC)
+#pragma unroll
+                    for (int c = 0; c < NC; ++c)
+#pragma unroll
+                        for (int pl = 0; pl < 3; ++pl) xc[c][pl] = xn[c][pl];
+            }
+            if (j == T - 1)
+#pragma unroll
+                for (int c = 0; c < NC; ++c) epi(j, c);
+        }
+    }
+
+    template <int l>
+    static MPCD_DEV void layer(const WS<l> &w, char *lds, int wave, int lane)
+    {
+        hidden<l>([&](int j, int kc, const u32x4 (&x)[3], f32x4 acc) { return mfma_x3(w.v[j][kc], x, acc); }, lds, wave,
+                  lane);
+    }
+
+    template <int li>
+    static MPCD_DEV void layer_res(const Res &r, const Tail &t, char *lds, int wave, int lane)
+    {
+        hidden<RES_L0 + li>(
+            [&](int j, int kc, const u32x4 (&x)[3], f32x4 acc) {
+                const int g = (li * 2 + j) * 4 + kc;
+                if (g < RES_AG) return mfma_x3_agpr(r.a[g][0], r.a[g][1], r.a[g][2], x, acc);
+                return mfma_x3(t.v[g - RES_AG], x, acc);
+            },
+            lds, wave, lane);
+    }
+
+    // x (4 features) -> fp32 row in XB and the three bf16 planes layer 0 reads
+    static MPCD_DEV void store_x(char *lds, int cl, int n, const f32x4 &x)
+    {
+        *reinterpret_cast<f32x4 *>(lds + L::XB + (cl * L::SX + n) * 4) = x;
+        u32x2 p0, p1, p2;
+        split3(x, p0, p1, p2);
+        char *o = lds + L::S1 + cl * L::RS + n * 2;
+        *reinterpret_cast<u32x2 *>(o) = p0;
+        *reinterpret_cast<u32x2 *>(o + L::PL) = p1;
+        *reinterpret_cast<u32x2 *>(o + 2 * L::PL) = p2;
+    }
+
+    using FW = WS<13>;
+    // final layer: wave w -> n-tiles w + 4j, both column tiles (a candidate's two CFG rows in one lane); at
+    // D0 = 32 and 32 rows load_ws<13>'s SPL mapping (n-tile w & 1) gives waves 0, 1 the same tiles
+    static constexpr int NZT = TL<13>;
+
+    // final Linear (32 -> D0) + the denoise update (reference op order, mlp_x3.hip final_and_update)
+    static MPCD_DEV void final_and_update(const FW &f, char *lds, const MlpSampleArgs &p, const StepPlan &sp, int s,
+                                          int64_t cand0, const f32x4 (&nz)[NZT][NB], uint32_t (&am)[2], int wave,
+                                          int lane)
+    {
+        constexpr int T = NZT, NT = D0 / 16;
+        const int col = lane & 15, q = lane >> 4;
+        const float *bias = reinterpret_cast<const float *>(lds + L::BI + A::boff(13) * 4);
+        f32x4 acc[T][2];
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            const int nt = (NT % 4 == 0 || wave + 4 * j < NT) ? wave + 4 * j : 0;
+            acc[j][0] = acc[j][1] = *reinterpret_cast<const f32x4 *>(bias + nt * 16 + 4 * q);
+        }
+#pragma unroll
+        for (int c = 0; c < NCT; ++c) {
+            u32x4 x[3];
+            load_x3(x, lds + L::T1 + (c * 16 + col) * L::RS + 8 * q * 2, L::PL);
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+                if (NT % 4 == 0 || wave + 4 * j < NT) acc[j][c] = mfma_x3(f.v[j][0], x, acc[j][c]);
+        }
+        if (R == 16 && NB == 2) {
+            // column c holds candidate c & 7's context row (c < 8) or masked row (c >= 8): bring the masked
+            // row's eps next to the context row's (DPP row_ror:8 swaps the two halves of each 16-lane row)
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float e = acc[j][0][r];  // element to a scalar first (bit_cast of a vector element)
+                    acc[j][1][r] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                        0, __builtin_bit_cast(int, e), 0x128, 0xF, 0xF, false));
+                }
+            if (col >= 8) return;  // lanes of the masked rows: their eps went to lane col - 8
+        }
+        const bool last = s == p.n_steps - 1;
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            const int nt = wave + 4 * j;
+            if (NT % 4 != 0 && nt >= NT) continue;
+            const int n = nt * 16 + 4 * q;
+#pragma unroll
+            for (int g = 0; g < (NB == 2 ? 1 : NCT); ++g) {
+                const int cl = NB == 2 ? col : g * 16 + col;
+                const f32x4 ec = acc[j][NB == 2 ? 0 : g];
+                const f32x4 eu = acc[j][1];
+                const int64_t gc = cand0 + cl;
+                if (SMODE == MODE_EPS || SMODE == MODE_EPS1) {
+                    if (gc < p.batch) {
+                        *reinterpret_cast<f32x4 *>(p.x_out + (size_t)gc * D0 + n) = ec;
+                        if (SMODE == MODE_EPS) *reinterpret_cast<f32x4 *>(p.chain + (size_t)gc * D0 + n) = eu;
+                    }
+                    continue;
+                }
+                const f32x4 x = *reinterpret_cast<const f32x4 *>(lds + L::XB + (cl * L::SX + n) * 4);
+                f32x4 xn;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float xv = x[r];
+                    float o;
+                    if (IS_DDPM) {
+                        const float x0c = sp.a * xv - sp.b * ec[r];
+                        const float x0u = sp.a * xv - sp.b * eu[r];
+                        float x0 = p.wp1 * x0c - p.wf * x0u;
+                        x0 = clamp1(x0);
+                        const float mean = sp.c1 * x0 + sp.c2 * xv;
+                        o = (sp.flags & PLAN_NOISE) ? mean + sp.std * nz[j][0][r] : mean;
+                    } else if (SMODE == MODE_DDIM_CFG) {
+                        float x0 = p.wp1 * (sp.a * xv - sp.b * ec[r]) - p.wf * (sp.a * xv - sp.b * eu[r]);
+                        if (p.clamp_x0) x0 = clamp1(x0);
+                        const float e = p.wp1 * ec[r] - p.wf * eu[r];
+                        o = (sp.flags & PLAN_FINAL) ? x0 : x0 * sp.sqan + sp.cn * e;
+                    } else {  // MODE_DDIM, 3-arg net
+                        float x0 = sp.a * xv - sp.b * ec[r];
+                        if (p.clamp_x0) x0 = clamp1(x0);
+                        o = (sp.flags & PLAN_FINAL) ? x0 : x0 * sp.sqan + sp.cn * ec[r];
+                    }
+                    xn[r] = o;
+                    am[g] = max(am[g], max(abs_bits(xv), abs_bits(o)));
+                }
+                store_x(lds, cl, n, xn);
+                if (gc < p.batch) {
+                    if (p.chain) *reinterpret_cast<f32x4 *>(p.chain + ((size_t)(s + 1) * p.batch + gc) * D0 + n) = xn;
+                    if (last) *reinterpret_cast<f32x4 *>(p.x_out + (size_t)gc * D0 + n) = xn;
+                }
+            }
+        }
+    }
+
+    // noise of step s (slice s+1) for this lane's quads, fetched one step ahead of use
+    static MPCD_DEV void fetch_noise(f32x4 (&nz)[NZT][NB], const MlpSampleArgs &p, const StepPlan &sp, int s,
+                                     int64_t cand0, int wave, int lane)
+    {
+        constexpr int NT = D0 / 16;
+#pragma unroll
+        for (int j = 0; j < NZT; ++j)
+#pragma unroll
+            for (int g = 0; g < NB; ++g) nz[j][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (!IS_DDPM || !(sp.flags & PLAN_NOISE)) return;  // DDIM: sigma = 0
+        const int col = lane & 15, q = lane >> 4;
+#pragma unroll
+        for (int j = 0; j < NZT; ++j) {
+            const int nt = wave + 4 * j;
+            if (NT % 4 != 0 && nt >= NT) continue;
+            const int n = nt * 16 + 4 * q;
+            const int64_t gc = cand0 + col;  // DDPM-CFG: NB == 2, one candidate per column (R = 16: columns < 8)
+            if (gc >= p.batch || (R == 16 && col >= 8)) continue;
+            if (SMODE == MODE_DDPM_XN)
+                nz[j][0] = *reinterpret_cast<const f32x4 *>(p.noise + ((size_t)(s + 1) * p.batch + gc) * D0 + n);
+            else
+                nz[j][0] = philox_normal4(p.seed, (uint64_t)(p.global_offset + gc), (uint32_t)(s + 1), (uint32_t)(n >> 2));
+        }
+    }
+
+    static MPCD_DEV void run(const MlpSampleArgs &p)
+    {
+        extern __shared__ float lds_f[];
+        char *lds = reinterpret_cast<char *>(lds_f);
+        const int lane = threadIdx.x & 63;
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const int64_t cand0 = (int64_t)blockIdx.x * CPW;
+        int lane16 = lane * 16;
+        const float *wp = p.wpack;
+        float *bi = reinterpret_cast<float *>(lds + L::BI);
+        float *bic = reinterpret_cast<float *>(lds + L::BIC);
+        float *cps = reinterpret_cast<float *>(lds + L::CPS);
+
+        Res res;
+        load_res(res, wp, wave, lane);
+        for (int l = 0; l < NLAYER; ++l)
+            for (int i = threadIdx.x; i < A::N[l]; i += RW_T) bi[A::boff(l) + i] = wp[woffx<D0>(l) + wfl<D0>(l) + i];
+        for (int j = 0; j < 6; ++j)
+            for (int i = threadIdx.x; i < A::N[2 * j + 1]; i += RW_T)
+                bic[cond_off(j) + i] = wp[woffx<D0>(2 * j + 1) + wfl<D0>(2 * j + 1) + i];
+        for (int i = threadIdx.x; i < COND_TOTAL; i += RW_T) cps[i] = CTX ? p.cproj[i] : 0.f;
+        if (threadIdx.x < CPW) reinterpret_cast<uint32_t *>(lds + L::AMX)[threadIdx.x] = 0u;
+        uint32_t am[2] = {0u, 0u};
+        for (int i = threadIdx.x; i < CPW * QUADS; i += RW_T) {  // x_T (fp32 + planes)
+            const int c = i / QUADS, qd = i - c * QUADS;
+            const int64_t gc = cand0 + c;
+            f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (gc < p.batch) {
+                z = p.noise ? *reinterpret_cast<const f32x4 *>(p.noise + (size_t)gc * D0 + qd * 4)
+                            : philox_normal4(p.seed, (uint64_t)(p.global_offset + gc), 0u, (uint32_t)qd);
+                if (p.chain && SMODE != MODE_EPS) *reinterpret_cast<f32x4 *>(p.chain + (size_t)gc * D0 + qd * 4) = z;
+            }
+            store_x(lds, c, qd * 4, z);
+        }
+
+        int wofs = 0;
+        WS<0> w0;
+        load_ws<0>(w0, wp, wave, lane16);
+        f32x4 nz[NZT][NB];
+        StepPlan sp = load_plan(p.plan, 0);
+        fetch_noise(nz, p, sp, 0, cand0, wave, lane);
+        const int tpi = threadIdx.x < COND_TOTAL / 4 ? (int)threadIdx.x : 0;
+        f32x4 tpre = reinterpret_cast<const f32x4 *>(p.tproj)[tpi];
+        auto bar = [] { lds_barrier(); };
+
+        for (int s = 0; s < p.n_steps; ++s) {
+            // launder the weight base: stops LICM hoisting the streamed layers' loads out of the loop
+            asm volatile("" : "+s"(wofs), "+v"(lane16));
+            const float *ws = wp + wofs;
+            WS<1> w1;
+            load_ws<1>(w1, ws, wave, lane16);
+            WS<2> w2;
+            load_ws<2>(w2, ws, wave, lane16);
+            bar();
+            // this step's time projections + cond biases (+ shared context part) -> TPU / TPC
+            if (threadIdx.x < COND_TOTAL / 4) {
+                const f32x4 u = tpre + reinterpret_cast<const f32x4 *>(lds + L::BIC)[tpi];
+                reinterpret_cast<f32x4 *>(lds + L::TPU)[tpi] = u;
+                reinterpret_cast<f32x4 *>(lds + L::TPC)[tpi] = u + reinterpret_cast<const f32x4 *>(lds + L::CPS)[tpi];
+            }
+            tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 1 < p.n_steps ? s + 1 : s) * COND_TOTAL)[tpi];
+            layer<0>(w0, lds, wave, lane);
+            WS<3> w3;
+            load_ws<3>(w3, ws, wave, lane16);
+            bar();
+            layer<1>(w1, lds, wave, lane);
+            WS<4> w4;
+            load_ws<4>(w4, ws, wave, lane16);
+            bar();
+            layer<2>(w2, lds, wave, lane);
+            bar();
+            layer<3>(w3, lds, wave, lane);
+            bar();
+            layer<4>(w4, lds, wave, lane);
+            bar();
+            Tail tail;
+            layer_res<0>(res, tail, lds, wave, lane);
+            // register budget (one wave per SIMD, 512 registers, 252 AGPRs hold resident weights): each layer's
+            // fragments are issued as late as the L2 latency allows - L8's 96 registers two layers ahead
+            WS<8> w8;
+            load_ws<8>(w8, ws, wave, lane16);
+            bar();
+            layer_res<1>(res, tail, lds, wave, lane);
+            load_tail(tail, ws, wave, lane16);
+            bar();
+            layer_res<2>(res, tail, lds, wave, lane);
+            WS<9> w9;
+            load_ws<9>(w9, ws, wave, lane16);
+            bar();
+            layer<8>(w8, lds, wave, lane);
+            WS<10> w10;
+            load_ws<10>(w10, ws, wave, lane16);
+            bar();
+            layer<9>(w9, lds, wave, lane);
+            WS<11> w11;
+            load_ws<11>(w11, ws, wave, lane16);
+            WS<12> w12;
+            load_ws<12>(w12, ws, wave, lane16);
+            WS<13> w13;
+            load_ws<13>(w13, ws, wave, lane16);
+            bar();
+            layer<10>(w10, lds, wave, lane);
+            const StepPlan cur = sp;
+            f32x4 nzc[NZT][NB];
+#pragma unroll
+            for (int j = 0; j < NZT; ++j)
+#pragma unroll
+                for (int g = 0; g < NB; ++g) nzc[j][g] = nz[j][g];
+            if (s + 1 < p.n_steps) {
+                sp = load_plan(p.plan, s + 1);
+                fetch_noise(nz, p, sp, s + 1, cand0, wave, lane);
+            }
+            load_ws<0>(w0, ws, wave, lane16);  // next step's layer 0 (unconditional: path-independent load count)
+            bar();
+            layer<11>(w11, lds, wave, lane);
+            bar();
+            layer<12>(w12, lds, wave, lane);
+            bar();
+            final_and_update(w13, lds, p, cur, s, cand0, nzc, am, wave, lane);
+        }
+        if (SMODE != MODE_EPS && SMODE != MODE_EPS1 && p.chain_absmax) {
+            const int col = lane & 15;
+            store_chain_absmax<CPW, RW_T>(reinterpret_cast<uint32_t *>(lds + L::AMX), am, col,
+                                          (NB == 2 || R == 16) ? -1 : 16 + col, NB == 1 || R == 32 || col < 8,
+                                          p.chain_absmax, cand0, p.batch);
+        }
+    }
+};
+
+template <int D0, int SMODE, bool CTX, int R>
+__global__ __launch_bounds__(RW_T, 1) void mlp_rw_kernel(const MlpSampleArgs p)
+{
+    MlpRw<D0, SMODE, CTX, R>::run(p);
+}
+
+template <int D0, int SMODE, bool CTX, int R>
+hipError_t launch_rw_r(const MlpSampleArgs &a, hipStream_t stream)
+{
+    using L = Lds3<D0, MlpRw<D0, SMODE, CTX, R>::NB, R>;
+    static_assert(L::total <= 160 * 1024, "LDS budget (160 KiB per CU)");
+    if (hipError_t e = allow_max_lds<&mlp_rw_kernel<D0, SMODE, CTX, R>>(); e != hipSuccess) return e;
+    const int64_t blocks = (a.batch + L::CPW - 1) / L::CPW;
+    hipLaunchKernelGGL((mlp_rw_kernel<D0, SMODE, CTX, R>), dim3((unsigned)blocks), dim3(RW_T), (size_t)L::total, stream, a);
+    return hipGetLastError();
+}
+
+template <int D0, int SMODE, bool CTX>
+hipError_t launch_rw(const MlpSampleArgs &a, int rows, hipStream_t stream)
+{
+    return rows == 16 ? launch_rw_r<D0, SMODE, CTX, 16>(a, stream) : launch_rw_r<D0, SMODE, CTX, 32>(a, stream);
+}
+
+template <int D0>
+hipError_t launch_rw_d0(const MlpSampleArgs &a, int rows, hipStream_t stream)
+{
+    const bool ctx = a.cproj != nullptr;
+    switch (a.mode) {
+    case MODE_DDPM_CFG:
+        if (a.noise) return ctx ? launch_rw<D0, MODE_DDPM_XN, true>(a, rows, stream) : launch_rw<D0, MODE_DDPM_XN, false>(a, rows, stream);
+        return ctx ? launch_rw<D0, MODE_DDPM_CFG, true>(a, rows, stream) : launch_rw<D0, MODE_DDPM_CFG, false>(a, rows, stream);
+    case MODE_DDIM_CFG: return ctx ? launch_rw<D0, MODE_DDIM_CFG, true>(a, rows, stream) : launch_rw<D0, MODE_DDIM_CFG, false>(a, rows, stream);
+    case MODE_DDIM: return ctx ? launch_rw<D0, MODE_DDIM, true>(a, rows, stream) : launch_rw<D0, MODE_DDIM, false>(a, rows, stream);
+    case MODE_EPS: return ctx ? launch_rw<D0, MODE_EPS, true>(a, rows, stream) : launch_rw<D0, MODE_EPS, false>(a, rows, stream);
+    case MODE_EPS1: return ctx ? launch_rw<D0, MODE_EPS1, true>(a, rows, stream) : launch_rw<D0, MODE_EPS1, false>(a, rows, stream);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+// rows: 32 or 16 per workgroup (mlp_x3.hip picks, as for its own layouts)
+hipError_t launch_mlp_rw(int d0, int rows, const MlpSampleArgs &a, hipStream_t stream)
+{
+    switch (d0) {
+    case 32: return launch_rw_d0<32>(a, rows, stream);
+    case 64: return launch_rw_d0<64>(a, rows, stream);
+    case 128: return launch_rw_d0<128>(a, rows, stream);
+    }
+    return hipErrorInvalidValue;
+}

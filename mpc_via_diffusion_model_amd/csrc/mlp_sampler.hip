@@ -198,10 +198,10 @@ MPCD_DEV void hidden_layer(const WFrag<K, N, MODE> &f, const float *init, const 
         }
 #ifndef MPCD_DIAG_NOMISH
         if (EPI != EPI_NONE) {
-            v.x = mish(v.x);
-            v.y = mish(v.y);
-            v.z = mish(v.z);
-            v.w = mish(v.w);
+            v.x = mish_scalar(v.x);
+            v.y = mish_scalar(v.y);
+            v.z = mish_scalar(v.z);
+            v.w = mish_scalar(v.w);
         }
 #endif
         *reinterpret_cast<f32x4 *>(out + (size_t)(ct * 16 + col) * out_stride + n) = v;

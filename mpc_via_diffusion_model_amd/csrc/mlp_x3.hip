@@ -26,273 +26,10 @@
 
 #include <atomic>
 
-#include "internal.h"
-#include "mlp_common.h"
+#include "mlp_x3.h"
 
 namespace {
-using namespace mlpc;
-
-// Rows per workgroup: 32 (16 candidates x {context, masked} for CFG) or, for batches too small to give
-// every CU a workgroup, 16 (8 candidates x 2): one 16-column MFMA tile per layer, half the MFMAs per
-// wave and per step, twice the workgroups (mlp_x3_layout() picks).
-constexpr int ROWS_MAX = 32;
-// WAVES = 8 (two per SIMD): while one wave of a SIMD waits on a barrier, an LDS read or its own
-// MFMA chain, the other issues, and a bf16 MFMA leaves vector issue free for 8 of its 16 cycles, so
-// one wave's Mish / split VALU runs under the other's MFMAs. Hidden layers then map as PAIR8
-// (N = 128: wave w -> n-tile w, both column tiles) or WIDE8 (N <= 64: wave w -> column tile w >> 2,
-// n-tiles (w & 3) + 4j); the final layer, which pairs a candidate's two CFG rows, runs on waves 0-3
-// in the PAIRED form. WAVES = 4 keeps the one-wave-per-SIMD schedule (hidden()).
-#ifndef MPCD_X3_WAVES
-#define MPCD_X3_WAVES 8
-#endif
-// MPCD_X3_ILV = 1: the N = 128 layers overlap one column tile's epilogue with the other's MFMAs
-// MPCD_X3_PAIR_MIN: narrowest layer mapped PAIR8 at 32 rows (each weight fragment loaded by one wave)
-#ifndef MPCD_X3_PAIR_MIN
-#define MPCD_X3_PAIR_MIN 128
-#endif
-#ifndef MPCD_X3_LEAD2
-#define MPCD_X3_LEAD2 0
-#endif
-#ifndef MPCD_X3_XALL
-#define MPCD_X3_XALL 0
-#endif
-#ifndef MPCD_X3_ILV
-#define MPCD_X3_ILV 1
-#endif
-// Experiment switches, all off in the product build (profiles/r3_mlp_vmem_ab.txt: every one measured slower):
-// MPCD_X3_WF32 fp32 weight stream split in registers (unfinished: also fails the cfg1 headline parity test),
-// MPCD_X3_SKIP_IDLE 1/2 idle waves issue no weight loads (branch / lane mask), MPCD_X3_EXP_NOPL2 timing probe
-// with the third weight plane's loads not issued (wrong results).
-#ifndef MPCD_X3_WF32
-#define MPCD_X3_WF32 0
-#endif
-#ifndef MPCD_X3_SKIP_IDLE
-#define MPCD_X3_SKIP_IDLE 0
-#endif
-#ifndef MPCD_X3_EXP_NOPL2
-#define MPCD_X3_EXP_NOPL2 0
-#endif
-constexpr int THREADS = 64 * MPCD_X3_WAVES;
-constexpr int WAVES = THREADS / 64;
-enum { SPLIT = 0, PAIRED = 1, WIDE8 = 2, PAIR8 = 3 };
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-// two fp32 -> two bf16 (round to nearest even), packed: v_cvt_pk_bf16_f32
-MPCD_DEV uint32_t pk_bf16(float lo, float hi)
-{
-    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, bf16x2));
-}
-MPCD_DEV float bf_lo(uint32_t p) { return __builtin_bit_cast(float, p << 16); }
-MPCD_DEV float bf_hi(uint32_t p) { return __builtin_bit_cast(float, p & 0xffff0000u); }
-
-// 4 consecutive fp32 features -> three bf16 planes (4 bf16 each): v = p0 + p1 + p2 (+ < 2^-27 |v|).
-// Each remainder v - bf16(v) is exact in fp32.
-MPCD_DEV void split3(const f32x4 &v, u32x2 &p0, u32x2 &p1, u32x2 &p2)
-{
-    const uint32_t a = pk_bf16(v.x, v.y), b = pk_bf16(v.z, v.w);
-    const f32x4 r = v - f32x4{bf_lo(a), bf_hi(a), bf_lo(b), bf_hi(b)};
-    const uint32_t c = pk_bf16(r.x, r.y), d = pk_bf16(r.z, r.w);
-    const f32x4 r2 = r - f32x4{bf_lo(c), bf_hi(c), bf_lo(d), bf_hi(d)};
-    p0 = u32x2{a, b};
-    p1 = u32x2{c, d};
-    p2 = u32x2{pk_bf16(r2.x, r2.y), pk_bf16(r2.z, r2.w)};
-}
-
-// ---- LDS layout (bytes). Activation buffers hold three bf16 planes of ROWS rows; a row stride of
-// 16 mod 256 bytes keeps the 16-lane groups of a ds_read_b128 conflict-free (MI355X_MICROARCH LDS
-// table: lane (q, col) reads 16 B at row col, chunk q).
-template <int D0, int NB, int ROWS>
-struct Lds3 {
-    static constexpr int CPW = ROWS / NB;  // candidates per workgroup
-    static constexpr int RS = 272;         // row stride, widths <= 128
-    static constexpr int RS2 = 528;        // row stride, width 256
-    static constexpr int PL = ROWS * RS, PL2 = ROWS * RS2;  // plane strides
-    static constexpr int SX = D0 + 4;      // fp32 x row stride (floats)
-    static constexpr int T1 = 0;
-    static constexpr int S1 = T1 + 3 * PL;  // also the x planes (layer-0 input) between steps
-    static constexpr int C1 = S1 + 3 * PL;
-    static constexpr int C0 = C1 + 3 * PL;
-    static constexpr int XB = C0 + 3 * PL2;                       // fp32 x [CPW][SX]
-    static constexpr int TPC = XB + CPW * SX * 4;                 // fp32 [448]: tproj + cond bias + shared cproj
-    static constexpr int TPU = TPC + COND_TOTAL * 4;              // fp32 [448]: tproj + cond bias
-    static constexpr int BIC = TPU + COND_TOTAL * 4;              // fp32 [448]: cond-layer biases
-    static constexpr int CPS = BIC + COND_TOTAL * 4;              // fp32 [448]: shared cproj (0 without context)
-    static constexpr int BI = CPS + COND_TOTAL * 4;               // fp32 all 14 biases
-    static constexpr int AMX = BI + Arch<D0>::btotal() * 4;       // uint32 [CPW]: chain |x| maxima
-    static constexpr int total = AMX + ROWS * 4;
-    static_assert(D0 * 2 + 16 <= RS, "x planes fit a 272-byte row");
-
-    // layer l: input / output buffer (byte offset incl. the feature offset of a concat half) and stride
-    static constexpr int in_off(int l) {
-        constexpr int t[NLAYER] = {S1, T1, S1, T1, C1 + 128, T1, C0 + 256, T1, C0, T1, C1, T1, S1, T1};
-        return t[l];
-    }
-    static constexpr int in_rs(int l) { return (l == 6 || l == 8) ? RS2 : RS; }
-    static constexpr int in_pl(int l) { return (l == 6 || l == 8) ? PL2 : PL; }
-    static constexpr int out_off(int l) {
-        constexpr int t[NLAYER] = {T1, S1, T1, C1 + 128, T1, C0 + 256, T1, C0, T1, C1, T1, S1, T1, 0};
-        return t[l];
-    }
-    static constexpr int out_rs(int l) { return (l == 5 || l == 7) ? RS2 : RS; }
-    static constexpr int out_pl(int l) { return (l == 5 || l == 7) ? PL2 : PL; }
-};
-
-// W = 4 with R = 16 (two workgroups per CU, see mlp_x3_layout): every layer PAIRED (wave w -> n-tiles w + 4j)
-template <int N, int R = 32, int W = WAVES>
-constexpr int mode_for()
-{
-    return W == 8 ? ((N >= MPCD_X3_PAIR_MIN || R == 16) ? PAIR8 : WIDE8) : R == 16 ? PAIRED : N == 32 ? SPLIT : PAIRED;
-}
-
-constexpr int epi_of(int l) { return l == 12 ? EPI_NONE : (l % 2 == 1) ? EPI_CMISH : EPI_MISH; }
-
-// Weight fragments of one layer for this wave: [T n-tiles][KC = K/32 k-chunks][3 planes], 16 bytes
-// (8 bf16) per lane each = the A operand of one v_mfma_f32_16x16x32_bf16.
-template <int K, int N, int MODE>
-struct WFrag3 {
-    static constexpr int NT = N / 16;
-    static constexpr int T = MODE == SPLIT ? NT / 2 : MODE == PAIR8 ? (NT + 7) / 8 : (NT + 3) / 4;  // n-tiles per wave
-    static constexpr int KC = K / 32;
-    u32x4 v[T][KC][3];
-};
-
-// What one wave loads for a layer: per (n-tile, k-chunk) WPL 16-byte pieces per lane — the three bf16
-// planes, or (MPCD_X3_WF32) the 8 fp32 weights as two halves, split into the planes in registers right
-// before the layer (to_planes: the same round-to-nearest-even split the host does, so the MFMA operands
-// are bit-identical) — 4 instead of 6 bytes per weight streamed from L2 every step.
-constexpr int WPL = MPCD_X3_WF32 ? 2 : 3;
-template <int K, int N, int MODE>
-struct WLoad {
-    using F = WFrag3<K, N, MODE>;
-    static constexpr int NT = F::NT, T = F::T, KC = F::KC;
-    u32x4 v[T][KC][WPL];
-};
-
-template <int K, int N, int MODE>
-MPCD_DEV void to_planes(const WLoad<K, N, MODE> &w, WFrag3<K, N, MODE> &f)
-{
-#pragma unroll
-    for (int j = 0; j < WFrag3<K, N, MODE>::T; ++j)
-#pragma unroll
-        for (int kc = 0; kc < WFrag3<K, N, MODE>::KC; ++kc) {
-            if constexpr (WPL == 3) {
-#pragma unroll
-                for (int pl = 0; pl < 3; ++pl) f.v[j][kc][pl] = w.v[j][kc][pl];
-            } else {
-                u32x2 a0, a1, a2, b0, b1, b2;
-                split3(__builtin_bit_cast(f32x4, w.v[j][kc][0]), a0, a1, a2);
-                split3(__builtin_bit_cast(f32x4, w.v[j][kc][1]), b0, b1, b2);
-                f.v[j][kc][0] = u32x4{a0.x, a0.y, b0.x, b0.y};
-                f.v[j][kc][1] = u32x4{a1.x, a1.y, b1.x, b1.y};
-                f.v[j][kc][2] = u32x4{a2.x, a2.y, b2.x, b2.y};
-            }
-        }
-}
-
-// packed floats per layer (weights, then the N fp32 biases) and layer offsets in the x3 pack
-template <int D0>
-constexpr int wfl(int l) { return WPL * Arch<D0>::K[l] * Arch<D0>::N[l] / 2; }
-template <int D0>
-constexpr int woffx(int l)
-{
-    int o = 0;
-    for (int i = 0; i < l; ++i) o += wfl<D0>(i) + Arch<D0>::N[i];
-    return o;
-}
-
-template <int K, int N, int MODE>
-MPCD_DEV int ntile_of(int wave, int j)
-{
-    return MODE == SPLIT ? (wave >> 1) + 2 * j : MODE == PAIR8 ? wave + 8 * j : (wave & 3) + 4 * j;
-}
-
-// One wave-uniform buffer descriptor per layer; chunk (nt, kc, plane) at soffset ((nt*KC+kc)*3+p) KiB.
-template <int K, int N, int MODE>
-MPCD_DEV void load_w3(WLoad<K, N, MODE> &f, const float *__restrict__ wp, int wave, int lane16, bool need = true)
-{
-    using F = WLoad<K, N, MODE>;
-    constexpr int KC = F::KC, NT = F::NT;
-    const uint64_t a = (uint64_t)wp;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(WPL * K * N * 2), 0x00020000);
-#pragma unroll
-    for (int j = 0; j < F::T; ++j) {
-        const int nt = min(ntile_of<K, N, MODE>(wave, j), NT - 1);
-#if MPCD_X3_SKIP_IDLE == 2
-        // A wave with no tile n (or need = false) runs its loads with every lane masked off: the
-        // instructions stay on every path (no control flow, so no vmcnt drain at a join) but move no data
-        const int lim = (need && ntile_of<K, N, MODE>(wave, j) < NT) ? 64 * 16 : 0;
-#pragma unroll
-        for (int kc = 0; kc < KC; ++kc)
-#pragma unroll
-            for (int pl = 0; pl < WPL; ++pl) {
-                const int soff = __builtin_amdgcn_readfirstlane(((nt * KC + kc) * WPL + pl) * 1024);
-                u32x4 v = u32x4{0u, 0u, 0u, 0u};
-                if (lane16 < lim) v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
-                f.v[j][kc][pl] = v;
-            }
-        continue;
-#elif MPCD_X3_SKIP_IDLE
-        // A wave with no tile n (or that does not run the layer: need = false) issues no loads. The
-        // vector-memory pipe, not the L2, is what the weight stream saturates: every 16-byte-per-lane
-        // load costs a CU the same issue time whether or not its data is used (profiles/r3_mlp_vmem_ab.txt).
-        if (!need || ntile_of<K, N, MODE>(wave, j) >= NT) {
-#pragma unroll
-            for (int kc = 0; kc < KC; ++kc)
-#pragma unroll
-                for (int pl = 0; pl < WPL; ++pl) f.v[j][kc][pl] = u32x4{0u, 0u, 0u, 0u};
-            continue;
-        }
-#else
-        // clamped, not skipped: the load count stays path-independent; a wave with no tile n uses
-        // nothing it loaded
-        (void)need;
-#endif
-#pragma unroll
-        for (int kc = 0; kc < KC; ++kc)
-#pragma unroll
-            for (int pl = 0; pl < WPL; ++pl) {
-                const int soff = __builtin_amdgcn_readfirstlane(((nt * KC + kc) * WPL + pl) * 1024);
-#if MPCD_X3_EXP_NOPL2
-                // timing experiment only (wrong results): the third plane's load not issued
-                f.v[j][kc][pl] = pl == 2 ? u32x4{0u, 0u, 0u, 0u} : __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
-#else
-                f.v[j][kc][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
-#endif
-            }
-    }
-}
-
-MPCD_DEV f32x4 mfma_bf(const u32x4 &a, const u32x4 &b, const f32x4 &c)
-{
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
-                                                   0);
-}
-
-// the six partial products of one 32-k chunk, smallest first
-MPCD_DEV f32x4 mfma_x3(const u32x4 (&w)[3], const u32x4 (&x)[3], f32x4 acc)
-{
-    acc = mfma_bf(w[2], x[0], acc);
-    acc = mfma_bf(w[1], x[1], acc);
-    acc = mfma_bf(w[0], x[2], acc);
-    acc = mfma_bf(w[1], x[0], acc);
-    acc = mfma_bf(w[0], x[1], acc);
-    acc = mfma_bf(w[0], x[0], acc);
-    return acc;
-}
-
-// activation fragment (3 planes) of row `row`, k-chunk kc: 16 bytes per plane per lane
-MPCD_DEV void load_x3(u32x4 (&x)[3], const char *base, int plane_stride)
-{
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl) x[pl] = *reinterpret_cast<const u32x4 *>(base + pl * plane_stride);
-}
+using namespace mlpx3;
 
 template <int D0, int SMODE, bool CTX, int R, int W = WAVES>
 struct MlpX3 {
@@ -362,10 +99,10 @@ struct MlpX3 {
             const int n = ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q;
             f32x4 v = acc[j][c];
             if (EPI != EPI_NONE) {
-                v.x = mish(v.x);
-                v.y = mish(v.y);
-                v.z = mish(v.z);
-                v.w = mish(v.w);
+                v.x = mish_scalar(v.x);
+                v.y = mish_scalar(v.y);
+                v.z = mish_scalar(v.z);
+                v.w = mish_scalar(v.w);
             }
             u32x2 p0, p1, p2;
             split3(v, p0, p1, p2);
@@ -432,10 +169,10 @@ struct MlpX3 {
             const int n = ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q;
             f32x4 v = acc[j][c];
             if (EPI != EPI_NONE) {
-                v.x = mish(v.x);
-                v.y = mish(v.y);
-                v.z = mish(v.z);
-                v.w = mish(v.w);
+                v.x = mish_scalar(v.x);
+                v.y = mish_scalar(v.y);
+                v.z = mish_scalar(v.z);
+                v.w = mish_scalar(v.w);
             }
             u32x2 p0, p1, p2;
             split3(v, p0, p1, p2);
@@ -855,7 +592,8 @@ hipError_t launch_x3_r(const MlpSampleArgs &a, hipStream_t stream)
 // Workgroup layout (rows x waves): 32x8 (one per CU), 16x8 when 32-row workgroups would leave CUs idle
 // (fewer than one per CU), 16x4 = two independent 4-wave workgroups per CU, whose barriers and
 // latency chains interleave on each SIMD instead of coinciding. MPCD_MLP_LAYOUT=32x8|16x8|16x4 forces.
-enum { LAYOUT_32x8 = 0, LAYOUT_16x8 = 1, LAYOUT_16x4 = 2 };
+// rw32 / rw16: mlp_rw.hip (4 waves, the 128-wide layers' weights resident in registers), 32 or 16 rows.
+enum { LAYOUT_32x8 = 0, LAYOUT_16x8 = 1, LAYOUT_16x4 = 2, LAYOUT_RW32 = 3, LAYOUT_RW16 = 4 };
 std::atomic<int> g_force_layout{-1};  // mpcd_mlp_force_layout (tests: every layout against the oracle)
 int mlp_x3_layout(int64_t batch, int nb)
 {
@@ -863,7 +601,8 @@ int mlp_x3_layout(int64_t batch, int nb)
     static const int forced = [] {
         const char *e = getenv("MPCD_MLP_LAYOUT");
         if (!e || !e[0]) return -1;
-        return !strcmp(e, "32x8") ? (int)LAYOUT_32x8 : !strcmp(e, "16x8") ? (int)LAYOUT_16x8 : !strcmp(e, "16x4") ? (int)LAYOUT_16x4 : -1;
+        return !strcmp(e, "32x8") ? (int)LAYOUT_32x8 : !strcmp(e, "16x8") ? (int)LAYOUT_16x8 : !strcmp(e, "16x4") ? (int)LAYOUT_16x4
+             : !strcmp(e, "rw32") ? (int)LAYOUT_RW32 : !strcmp(e, "rw16") ? (int)LAYOUT_RW16 : -1;
     }();
     if (forced >= 0) return forced;
     const int n_cu = device_cu_count();
@@ -871,10 +610,10 @@ int mlp_x3_layout(int64_t batch, int nb)
 }
 
 template <int D0, int SMODE, bool CTX>
-hipError_t launch_x3(const MlpSampleArgs &a, hipStream_t stream)
+hipError_t launch_x3(const MlpSampleArgs &a, int layout, hipStream_t stream)
 {
     constexpr int NB = MlpX3<D0, SMODE, CTX, 32>::NB;
-    switch (mlp_x3_layout(a.batch, NB)) {
+    switch (layout) {
     case LAYOUT_16x8: return launch_x3_r<D0, SMODE, CTX, 16, 8>(a, stream);
     case LAYOUT_16x4:  // where two 16-row workgroups fit the CU's LDS (else 16x8)
         if constexpr (2 * Lds3<D0, NB, 16>::total <= 160 * 1024) return launch_x3_r<D0, SMODE, CTX, 16, 4>(a, stream);
@@ -884,17 +623,17 @@ hipError_t launch_x3(const MlpSampleArgs &a, hipStream_t stream)
 }
 
 template <int D0>
-hipError_t launch_x3_d0(const MlpSampleArgs &a, hipStream_t stream)
+hipError_t launch_x3_d0(const MlpSampleArgs &a, int lay, hipStream_t stream)
 {
     const bool ctx = a.cproj != nullptr;
     switch (a.mode) {
     case MODE_DDPM_CFG:
-        if (a.noise) return ctx ? launch_x3<D0, MODE_DDPM_XN, true>(a, stream) : launch_x3<D0, MODE_DDPM_XN, false>(a, stream);
-        return ctx ? launch_x3<D0, MODE_DDPM_CFG, true>(a, stream) : launch_x3<D0, MODE_DDPM_CFG, false>(a, stream);
-    case MODE_DDIM_CFG: return ctx ? launch_x3<D0, MODE_DDIM_CFG, true>(a, stream) : launch_x3<D0, MODE_DDIM_CFG, false>(a, stream);
-    case MODE_DDIM: return ctx ? launch_x3<D0, MODE_DDIM, true>(a, stream) : launch_x3<D0, MODE_DDIM, false>(a, stream);
-    case MODE_EPS: return ctx ? launch_x3<D0, MODE_EPS, true>(a, stream) : launch_x3<D0, MODE_EPS, false>(a, stream);
-    case MODE_EPS1: return ctx ? launch_x3<D0, MODE_EPS1, true>(a, stream) : launch_x3<D0, MODE_EPS1, false>(a, stream);
+        if (a.noise) return ctx ? launch_x3<D0, MODE_DDPM_XN, true>(a, lay, stream) : launch_x3<D0, MODE_DDPM_XN, false>(a, lay, stream);
+        return ctx ? launch_x3<D0, MODE_DDPM_CFG, true>(a, lay, stream) : launch_x3<D0, MODE_DDPM_CFG, false>(a, lay, stream);
+    case MODE_DDIM_CFG: return ctx ? launch_x3<D0, MODE_DDIM_CFG, true>(a, lay, stream) : launch_x3<D0, MODE_DDIM_CFG, false>(a, lay, stream);
+    case MODE_DDIM: return ctx ? launch_x3<D0, MODE_DDIM, true>(a, lay, stream) : launch_x3<D0, MODE_DDIM, false>(a, lay, stream);
+    case MODE_EPS: return ctx ? launch_x3<D0, MODE_EPS, true>(a, lay, stream) : launch_x3<D0, MODE_EPS, false>(a, lay, stream);
+    case MODE_EPS1: return ctx ? launch_x3<D0, MODE_EPS1, true>(a, lay, stream) : launch_x3<D0, MODE_EPS1, false>(a, lay, stream);
     }
     return hipErrorInvalidValue;
 }
@@ -969,10 +708,12 @@ hipError_t launch_mlp_x3(int d0, int nb, const MlpSampleArgs &a, hipStream_t str
 {
     if ((nb == 1) != (a.mode == MODE_DDIM || a.mode == MODE_EPS1)) return hipErrorInvalidValue;
     if (a.cproj && a.cproj_stride != 0) return hipErrorInvalidValue;  // shared context only
+    const int lay = mlp_x3_layout(a.batch, nb);  // decided once per call
+    if (lay == LAYOUT_RW32 || lay == LAYOUT_RW16) return launch_mlp_rw(d0, lay == LAYOUT_RW32 ? 32 : 16, a, stream);
     switch (d0) {
-    case 32: return launch_x3_d0<32>(a, stream);
-    case 64: return launch_x3_d0<64>(a, stream);
-    case 128: return launch_x3_d0<128>(a, stream);
+    case 32: return launch_x3_d0<32>(a, lay, stream);
+    case 64: return launch_x3_d0<64>(a, lay, stream);
+    case 128: return launch_x3_d0<128>(a, lay, stream);
     }
     return hipErrorInvalidValue;
 }

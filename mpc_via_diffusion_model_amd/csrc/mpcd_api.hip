@@ -778,7 +778,8 @@ int mpcd_unet_form(mpcd_ctx *c, int32_t sampler, int32_t out[4])
 
 int mpcd_mlp_force_layout(int32_t layout)
 {
-    if (layout < -1 || layout > 2) return fail(MPCD_EINVAL, "layout -1 (auto), 0 (32x8), 1 (16x8) or 2 (16x4)");
+    if (layout < -1 || layout > 4)
+        return fail(MPCD_EINVAL, "layout -1 (auto), 0 (32x8), 1 (16x8), 2 (16x4), 3 (rw32) or 4 (rw16)");
     mlp_x3_force_layout(layout);
     return MPCD_OK;
 }

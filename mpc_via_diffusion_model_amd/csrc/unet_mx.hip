@@ -512,14 +512,13 @@ __device__ __forceinline__ void conv_mx_body(const ConvMK2 &as)
                     for (int e = 0; e < 4; ++e) {
                         const float scale = rstd * gw_t[e];
                         const float shift = -scale * mean + gb_t[e];
-                        v[e] = mish(raw[e] * scale + shift);
-                        // Keep each element's Mish in scalar VALU ops. Packed by hipcc's SLP vectorizer (ROCm
-                        // 7.2), the epilogue reads v_rcp_f32 results with v_pk_fma_f32 one wait state later (432
-                        // sites), and those builds give wrong conv outputs on the GPU; the same code without SLP
-                        // packing is exact (profiles/r3_hazard_ab.txt, tests/test_isa.py keeps the U-Net kernels
-                        // free of the pattern). This empty register fence per element costs ~2 % of the kernel.
+                        // Each element's Mish in scalar VALU ops (common.h mish_scalar: packed by hipcc's SLP
+                        // vectorizer, this epilogue read v_rcp_f32 results with v_pk_fma_f32 one wait state later
+                        // and gave wrong conv outputs on the GPU, profiles/r3_hazard_ab.txt). ~2 % of the kernel.
 #ifndef MPCD_MX_NO_FENCE
-                        asm volatile("" : "+v"(v[e]));
+                        v[e] = mish_scalar(raw[e] * scale + shift);
+#else
+                        v[e] = mish(raw[e] * scale + shift);
 #endif
                     }
                     if (epi == UEPI_GN_MISH_COND) {  // row < b_cand: context branch; else the masked (CFG) branch

@@ -59,12 +59,12 @@ def force_unet_path(path="auto"):
     N.check(N.lib().mpcd_unet_force_path(UNET_PATHS[path]), "mpcd_unet_force_path")
 
 
-MLP_LAYOUTS = {"auto": -1, "32x8": 0, "16x8": 1, "16x4": 2}
+MLP_LAYOUTS = {"auto": -1, "32x8": 0, "16x8": 1, "16x4": 2, "rw32": 3, "rw16": 4}
 
 
 def force_mlp_layout(layout="auto"):
     """Process-wide MLP sampler workgroup layout (mpcd_mlp_force_layout): "auto" (by batch size), "32x8",
-    "16x8" or "16x4" (rows x waves per workgroup)."""
+    "16x8" or "16x4" (rows x waves per workgroup), "rw32" / "rw16" (4 waves, resident 128-wide weights)."""
     N.check(N.lib().mpcd_mlp_force_layout(MLP_LAYOUTS[layout]), "mpcd_mlp_force_layout")
 
 

@@ -164,7 +164,7 @@ def test_f32x3_matches_exact_f32_at_full_size():
     assert float(rel.max()) < 1e-4, float(rel.max())
 
 
-@pytest.mark.parametrize("layout", ["32x8", "16x8", "16x4"])
+@pytest.mark.parametrize("layout", ["32x8", "16x8", "16x4", "rw32", "rw16"])
 def test_every_workgroup_layout_matches_oracle(layout):
     """Each split-bf16 sampler layout (mpcd_mlp_force_layout) against the oracle at the cfg1 shape and a ragged
     per-candidate-context batch, plus both CFG branches of one eps evaluation; the default picks 16x8 below one
@@ -197,3 +197,33 @@ def test_every_workgroup_layout_matches_oracle(layout):
         assert float((ec.cpu() - rc).abs().max()) <= 1e-5 and float((eu.cpu() - ru).abs().max()) <= 1e-5
     finally:
         force_mlp_layout("auto")
+
+
+@pytest.mark.parametrize("B,H,d,nwo,mode", [(4096, 32, 2, 0, "ddpm"), (1000, 16, 2, 5, "ddpm"), (300, 64, 2, 0, "ddpm"),
+                                           (257, 32, 2, 0, "ddim_cfg"), (96, 32, 2, 0, "ddim")])
+def test_every_workgroup_layout_bit_identical(B, H, d, nwo, mode):
+    """All five sampler layouts compute the same sums in the same order (include/mpcd.h mpcd_mlp_force_layout):
+    32x8, 16x8, 16x4 and the resident-weight rw32 / rw16 (csrc/mlp_rw.hip) give the same bits, Philox noise,
+    at the cfg2 shape and ragged batches, H*d = 32 / 64 / 128, CFG-DDPM with noise-free steps, CFG-DDIM and the
+    3-arg DDIM net."""
+    from mpc_via_diffusion_model_amd.planner import force_mlp_layout
+    C = 4
+    net = make_mlp(d, H, C, seed=5)
+    plan = _planner(net, d, H, C, 100, cfg=mode != "ddim", dtype="f32x3")
+    ctx = _ctx(B, C, True)
+    outs = {}
+    try:
+        for lay in ("32x8", "16x8", "16x4", "rw32", "rw16"):
+            force_mlp_layout(lay)
+            if mode == "ddpm":
+                outs[lay] = plan.run_CFG(ctx, None, 0.01, n_samples=B, horizon=H, return_chain=True,
+                                         n_diffusion_steps_without_noise=nwo, seed=3)
+            else:
+                outs[lay] = plan.sample_trajectories(ctx, B, H, seed=3, sample_fn=mode)
+            torch.cuda.synchronize()
+    finally:
+        force_mlp_layout("auto")
+    ref = outs["32x8"]
+    assert torch.isfinite(ref).all()
+    for lay, o in outs.items():
+        assert torch.equal(o, ref), f"{lay} differs from 32x8 ({mode}, B={B}, H={H}): max |d| {float((o - ref).abs().max()):.3e}"

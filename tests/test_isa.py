@@ -5,7 +5,8 @@
    (tests/test_gpu_unet_bench_sizes.py, bit-identity across tilings, failed with -DMPCD_MX_NO_FENCE and passed
    with the fence or with -fno-slp-vectorize: tools/hazard_ab.sh, profiles/r3_hazard_ab.txt). The only code
    difference: 432 sites where a v_pk_fma_f32 reads a v_rcp_f32 result one wait state after it. The U-Net
-   kernels must keep every packed reader of a transcendental result at >= 2 wait states.
+   same pattern sat in the MLP samplers' Mish epilogues (626 sites in round 3); every kernel of the library must
+   keep every packed reader of a transcendental result at >= 2 wait states.
 2. `__builtin_bit_cast` of an element of a builtin's ext-vector result reads element 0 (clang, ROCm 7.2):
    the permlane-swap reductions of csrc/unet_fused.hip copy the element to a scalar first."""
 import glob
@@ -39,15 +40,20 @@ def _disassemble(tmp_path):
     return "\n".join(text).splitlines()
 
 
-def test_unet_kernels_keep_packed_reads_of_transcendentals_two_wait_states_away(tmp_path):
+def test_every_kernel_keeps_packed_reads_of_transcendentals_two_wait_states_away(tmp_path):
+    """Every kernel of the shipped code object: the MLP samplers (mlp_x3_kernel is the cfg2 headline kernel), the
+    layer-by-layer and fused U-Nets, the prologues, the rollout and the training kernels."""
     import trans_hazard as th
     sites = th.scan(_disassemble(tmp_path))
-    unet = [s for s in sites if s[0] and ("conv_mx_kernel" in s[0] or "unet_fused_kernel" in s[0])]
-    assert any("unet_fused_kernel" in s[0] for s in unet), "fused U-Net kernel not found in the code object"
-    packed = [s for s in unet if s[4]]
+    kernels = {s[0] for s in sites if s[0]}
+    for k in ("unet_fused_kernel", "conv_mx_kernel", "mlp_x3_kernel", "mlp_sample_kernel"):
+        assert any(k in n for n in kernels), f"{k} not found in the code object"
+    packed = [s for s in sites if s[4]]
     close = [s for s in packed if s[3] < 2]
-    assert not close, f"{len(close)} packed reads of a transcendental result under 2 wait states: {close[:3]}"
-    assert packed, "the fused U-Net's packed Mish should read exp / rcp results (pattern not found: scan broken?)"
+    assert not close, (f"{len(close)} packed reads of a transcendental result under 2 wait states in "
+                       f"{len({s[0] for s in close})} kernels: {close[:3]}")
+    assert any("unet_fused_kernel" in s[0] for s in packed), \
+        "the fused U-Net's packed Mish should read exp / rcp results (pattern not found: scan broken?)"
 
 
 def test_scan_finds_the_one_wait_state_pattern():
