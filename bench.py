@@ -157,6 +157,69 @@ def cpu_baseline(cfg, budget_s=12.0):
                       f"process's share); per-candidate cost is linear in B, so cand/s at B={cfg['B']} is the same"}
 
 
+PANDA_CKPT = os.path.join(ROOT, "tests", "golden", "panda_test6_117600_ema.safetensors")
+PANDA_REF_S = 0.3615  # BASELINE.md / SURVEY §6: the reference's median Panda control step (unspecified CUDA GPU)
+
+
+def panda(args):
+    """The reference's one published timing: a Panda control step of
+    scripts/Panda/panda_inference/inference_diffusion_panda.py:118-120 / 436-450 - normalise the 20-dim state
+    (LimitsNormalizer, fp64 -> fp32), run_CFG(context, None, w=0.01, n_samples=1, horizon=128,
+    return_chain=True, ddpm_cart_pole_sample_fn, n_diffusion_steps_without_noise=5) with the trained
+    panda_test6_117600 EMA net (ConditionedTemporalUnet d=7, C=20, N=25, the checkpoint's schedule buffers),
+    timed host-side around the call and a stream synchronisation, as the reference's time.time() pair around
+    diffusion_sampling (its TimerCUDA synchronises). States ~ U[-1, 1]^20 with limits [-1, 1] (the training
+    data behind the reference's limits is not shipped). Also: the same step at B = 64 candidates (throughput)."""
+    from safetensors.torch import load_file
+
+    from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec
+    torch.cuda.set_device(0)
+    dtype = args.dtype or "f32x3"
+    sd = load_file(PANDA_CKPT)
+    plan = DiffusionMPC.from_state_dict(sd, NetSpec("unet", state_dim=7, horizon=128, context_dim=20, dtype=dtype))
+    rng = np.random.default_rng(1)
+    steps = args.steps if args.steps is not None else 200
+    warmup = args.warmup if args.warmup is not None else 10
+
+    def control_step(x, B, i):
+        ctx = plan.normalize_condition(x)[None]   # dataset.normalize_condition (host, fp64 -> fp32)
+        chain = plan.run_CFG(ctx, None, 0.01, n_samples=B, horizon=128, return_chain=True,
+                             n_diffusion_steps_without_noise=5, seed=i)
+        torch.cuda.synchronize()
+        return chain
+
+    out = {"metric": "Panda control-step latency (run_CFG, B=1, H=128, 25 + 5 CFG-DDPM steps, return_chain)",
+           "unit": "s", "higher_is_better": False, "n_gpus": 1, "steps": steps, "warmup": warmup,
+           "dtype": "f16" if dtype == "f16" else "f32", "data": "trained panda_test6_117600 EMA weights "
+           "(tests/golden), synthetic states ~ U[-1,1]^20", "vs_baseline": None,
+           "reference_published_s": {"median": PANDA_REF_S, "note": "BASELINE.md / SURVEY §6, unspecified CUDA GPU "
+                                     "(eager PyTorch); context only, different hardware"}}
+    for B in (1, 64):
+        xs = rng.uniform(-1, 1, (warmup + steps, 20))
+        for i in range(warmup):
+            control_step(xs[i], B, i)
+        lat, ker = [], []
+        for i in range(steps):
+            t0 = time.perf_counter()
+            chain = control_step(xs[warmup + i], B, warmup + i)
+            lat.append(time.perf_counter() - t0)
+            ker.append(plan.last_sample_ms())
+        assert tuple(chain.shape) == (31, B, 128, 7) and torch.isfinite(chain).all()
+        lat = np.array(lat)
+        rec = {"p50_s": float(np.median(lat)), "mean_s": float(lat.mean()), "min_s": float(lat.min()),
+               "max_s": float(lat.max()), "kernel_ms_mean": float(np.mean(ker)),
+               "candidates_per_s": B / float(np.median(lat))}
+        if B == 1:
+            out.update(value=rec["p50_s"], ms_per_step=1e3 * rec["p50_s"], latency_b1=rec)
+        else:
+            out["throughput_b64"] = rec
+    form = plan.unet_form("ddpm_cfg")
+    out["config"] = {"workload": "panda: trained ConditionedTemporalUnet d=7, C=20, H=128, N=25 + 5 noise-free, CFG w=0.01",
+                     "unet_form": form, "gemm": dtype}
+    out["cpu_baseline"] = None
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -164,13 +227,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=None, help="untimed control steps (default 20: the shader clock settles over the first dozen launches; U-Net configs 2, the first one runs the tiling autotune)")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong (SURVEY §8d: fixed B_total split over the ranks) or weak (B per rank)")
-    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS) + ["panda"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-shard-probe", action="store_true", help="skip the strong-scaling shard probes (kernel traces)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--dtype", default=None, choices=["f32", "f32x3", "f16"],
                     help="GEMM numerics: exact fp32 MFMA, fp32-accurate split-bf16 MFMA, fp16 operands (U-Net)")
     args = ap.parse_args()
+    if args.workload == "panda":
+        return panda(args)
     cfg = dict(WORKLOADS[args.workload])
     dtype = args.dtype or cfg["dtype"]
     unet = cfg["net"] == "unet"
@@ -257,8 +322,14 @@ def main():
         flops_launch = b_local * n_evals * 2 * 2 * cfg["mac"]   # survey's algorithmic count (fp32 FLOPs)
         achieved = flops_launch / (kms * 1e-3)
         if not unet:
-            kname = {"f32": "mlp_sample_kernel<%d,DDPM_CFG,ctx>", "f32x3": "mlp_x3_kernel<%d,DDPM_CFG,ctx>"}[dtype] % (
-                cfg["H"] * cfg["d"])
+            lay = plan.mlp_layout(b_local) if dtype == "f32x3" else None
+            if dtype == "f32":
+                kname = "mlp_sample_kernel<%d,DDPM_CFG,ctx>" % (cfg["H"] * cfg["d"])
+            elif lay.startswith("rw"):
+                kname = "mlp_rw_kernel<%d,DDPM_CFG,ctx,%s>" % (cfg["H"] * cfg["d"], lay[2:])
+            else:
+                r_, w_ = lay.split("x")
+                kname = "mlp_x3_kernel<%d,DDPM_CFG,ctx,%s,%s>" % (cfg["H"] * cfg["d"], r_, w_)
             timed = f"{kname}: the whole denoising loop in one persistent launch (HIP events on the call's stream)"
         else:
             form = plan.unet_form(cfg["sampler"])

@@ -342,6 +342,9 @@ int mpcd_unet_force_tiling(int32_t conv_pick, int32_t block_pick);
  * 128-wide layers' weights resident in registers for the whole launch). All layouts compute the same sums in
  * the same order (bit-identical results). */
 int mpcd_mlp_force_layout(int32_t layout);
+/* The layout (0..4 as above) an MPCD_F32X3 MLP sample call of `batch` candidates runs on the current device
+ * (cfg_masked: CFG net, two rows per candidate). */
+int mpcd_mlp_layout(int64_t batch, int32_t cfg_masked, int32_t *layout_out);
 /* U-Net execution form, process-wide. The whole-network form (csrc/unet_fused.hip: every conv of one denoise
  * step in ONE launch, a workgroup per few candidates, activations in LDS) covers the CFG samplers and the
  * two-branch eps of ConditionedTemporalUnet(base 32, dim_mults (1, 2, 4)) at H = 32 / 64 with the MPCD_F32X3

@@ -105,6 +105,7 @@ EXPORTS = {
     "mpcd_last_step_flags": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "mpcd_unet_force_tiling": ([ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
     "mpcd_mlp_force_layout": ([ctypes.c_int32], ctypes.c_int),
+    "mpcd_mlp_layout": ([ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "mpcd_unet_force_path": ([ctypes.c_int32], ctypes.c_int),
     "mpcd_unet_form": ([ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "mpcd_comm_init_loopback": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64], ctypes.c_int),

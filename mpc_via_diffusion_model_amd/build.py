@@ -83,7 +83,9 @@ def build(force=False, verbose=False, variant=None, defines=()):
         list(ex.map(run, jobs))
     objs = [os.path.join(obj, s.replace(".hip", ".o")) for s in SOURCES]
     if force or jobs or _stale(out, objs):
-        run([cc, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", out] + objs + LIBS)
+        tmp = out + ".tmp"  # link beside, then rename: a reader never sees a half-written library
+        run([cc, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", tmp] + objs + LIBS)
+        os.replace(tmp, out)
     return out
 
 

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "../../include/mpcd.h"
 #include "common.h"
 
@@ -29,16 +31,23 @@ hipError_t launch_philox_noise(uint64_t seed, int64_t goff, int64_t n, int n_sli
                                hipStream_t stream);
 
 // Thread-safe launch state (several host threads may launch, e.g. the loopback communicator's ranks):
-// allow_max_lds<&kernel>() raises the kernel's dynamic-LDS cap to 160 KiB exactly once per kernel (one
-// instantiation per kernel address; a C++11 function-local static initialiser runs once, whichever
-// thread gets there first, and the others wait for it); device_cu_count() is the compute-unit count of
-// the CURRENT device, cached per device.
+// allow_max_lds<&kernel>() raises the kernel's dynamic-LDS cap to 160 KiB exactly once per kernel and
+// device (the attribute belongs to the current device's copy of the function; a std::call_once per
+// device, whichever thread gets there first, the others wait for it); device_cu_count() is the
+// compute-unit count of the CURRENT device, cached per device.
+constexpr int kMaxDevices = 64;
 template <auto Kernel>
 inline hipError_t allow_max_lds()
 {
-    static const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(Kernel),
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    return e;
+    static std::once_flag once[kMaxDevices];
+    static hipError_t err[kMaxDevices];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+    std::call_once(once[dev], [dev] {
+        err[dev] = hipFuncSetAttribute(reinterpret_cast<const void *>(Kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       160 * 1024);
+    });
+    return err[dev];
 }
 int device_cu_count();
 
@@ -68,6 +77,7 @@ hipError_t launch_mlp_sampler(int d0, int nb, const MlpSampleArgs &a, hipStream_
 // fp32-accurate split-bf16 variant (mlp_x3.hip); shared or no context only
 int mlp_packed_floats_x3(int d0);
 void mlp_x3_force_layout(int layout);  // mpcd_mlp_force_layout
+int mlp_x3_layout_of(int64_t batch, int nb);  // mpcd_mlp_layout: the layout a call of this batch runs
 void mlp_pack_weights_x3(int d0, const float *const *lin_w, const float *const *lin_b, float *out);
 hipError_t launch_mlp_x3(int d0, int nb, const MlpSampleArgs &a, hipStream_t stream);
 // resident-weight variant (mlp_rw.hip), selected by mlp_x3's layout choice: rows = 32 or 16 per workgroup

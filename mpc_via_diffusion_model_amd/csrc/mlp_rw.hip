@@ -52,6 +52,32 @@ MPCD_DEV f32x4 mfma_x3_agpr(const u32x4 &w0, const u32x4 &w1, const u32x4 &w2, c
     return acc;
 }
 
+// partial product m of a 32-k chunk, smallest first (mlp_x3.h mfma_x3): weight plane, activation plane
+constexpr int wpl(int m) { return m == 0 ? 2 : (m == 1 || m == 3) ? 1 : 0; }
+constexpr int xpl(int m) { return (m == 0 || m == 3 || m == 5) ? 0 : (m == 1 || m == 4) ? 1 : 2; }
+
+// One partial product with the weight plane in an AGPR. NOP: the first MFMA of a chain, whose accumulator may
+// have just been written by a VALU op (2 wait states); inside a chain the accumulator comes from the previous
+// MFMA (srcC forwarding, no wait). tests/test_isa.py checks every MFMA source of the library for a VALU write
+// under 2 wait states.
+template <bool NOP>
+MPCD_DEV f32x4 mfma_agpr1(const u32x4 &w, const u32x4 &x, f32x4 acc)
+{
+    if constexpr (NOP)
+        asm("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(x));
+    else
+        asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(x));
+    return acc;
+}
+
+// MPCD_RW_ILV = 1: each hidden layer as a pipeline of passes (one n-tile x one column tile: a chain of 6 KC
+// MFMAs), the previous pass's epilogue (4 Mish, the split, 3 LDS stores) issued one unit after each of this
+// pass's first MFMAs (pinned with sched_barrier: a bf16 MFMA leaves the SIMD's vector issue free for 8 of its
+// 16 cycles), the next activation fragments read two k-chunks ahead; 0 = the plain form (hidden()).
+#ifndef MPCD_RW_ILV
+#define MPCD_RW_ILV 1
+#endif
+
 template <int D0, int SMODE, bool CTX, int R>
 struct MlpRw {
     static constexpr int NB = (SMODE == MODE_DDIM || SMODE == MODE_EPS1) ? 1 : 2;
@@ -215,16 +241,98 @@ struct MlpRw {
         }
     }
 
+    // Pipelined form of hidden(). MM1(j, kc, m, x[3], acc) -> acc: partial product m (0..5, smallest first:
+    // the mfma_x3 order) of k-chunk kc of n-tile j. Same products in the same order as hidden(): bit-identical.
+    template <int l, class MM1>
+    static MPCD_DEV void hidden_ilv(MM1 mm1, char *lds, int wave, int lane)
+    {
+        constexpr int K = A::K[l], N = A::N[l], KC = K / 32, NT = N / 16, T = TL<l>, NC = CL<l>, EPI = epi_of(l);
+        constexpr int NP = T * NC, NI = NP * KC;  // passes; (pass, k-chunk) steps
+        const int col = lane & 15, q = lane >> 4;
+        constexpr bool in_shared = l == 0 && NB == 2;  // CFG: both branches read the candidate's x
+        static_assert(T == 1 || NT % 4 == 0, "only a one-tile layer can leave a wave idle");
+        if constexpr (NT < 4 && !SPL<l>)
+            if (wave >= NT) return;  // N = 32 at 16 rows: waves 2, 3 have no tile
+        auto jp = [](int p) { return p / NC; };
+        auto cp = [](int p) { return p % NC; };
+        auto init_of = [&](int p) {
+            const int ct = ct_of<l>(wave, cp(p));
+            const float *init = reinterpret_cast<const float *>(
+                lds + (EPI == EPI_CMISH ? (masked_of(ct, col) ? L::TPU : L::TPC) + cond_off(l / 2) * 4
+                                        : L::BI + A::boff(l) * 4));
+            return *reinterpret_cast<const f32x4 *>(init + min(nt_of<l>(wave, jp(p)), NT - 1) * 16 + 4 * q);
+        };
+        auto ldx = [&](u32x4 (&x)[3], int i) {  // step i = (pass i / KC, k-chunk i % KC)
+            const int p = i / KC, kc = i % KC, ct = ct_of<l>(wave, cp(p));
+            const int row = in_shared ? cand_of(ct, col) : ct * 16 + col;
+            load_x3(x, lds + L::in_off(l) + row * L::in_rs(l) + (kc * 32 + 8 * q) * 2, L::in_pl(l));
+        };
+        // epilogue of pass p in five units: Mish of element 0..3, then the split + the three plane stores
+        auto epi_unit = [&](int u, f32x4 &v, int p) {
+            if (u < 4) {
+                if (EPI != EPI_NONE) v[u] = mish_scalar(v[u]);
+                return;
+            }
+            const int n = nt_of<l>(wave, jp(p)) * 16 + 4 * q;
+            u32x2 p0, p1, p2;
+            split3(v, p0, p1, p2);
+            char *o = lds + L::out_off(l) + (ct_of<l>(wave, cp(p)) * 16 + col) * L::out_rs(l) + n * 2;
+            *reinterpret_cast<u32x2 *>(o) = p0;
+            *reinterpret_cast<u32x2 *>(o + L::out_pl(l)) = p1;
+            *reinterpret_cast<u32x2 *>(o + 2 * L::out_pl(l)) = p2;
+        };
+        u32x4 xb[3][3];
+        ldx(xb[0], 0);
+        if (NI > 1) ldx(xb[1], 1);
+        f32x4 acc = init_of(0), nxt = acc, ev = acc;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            if (p + 1 < NP) nxt = init_of(p + 1);
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc) {
+                const int i = p * KC + kc;
+                if (i + 2 < NI) ldx(xb[(i + 2) % 3], i + 2);
+#pragma unroll
+                for (int m = 0; m < 6; ++m) {
+                    acc = mm1(jp(p), kc, m, xb[i % 3], acc);
+                    const int u = kc * 6 + m;
+                    if (p > 0 && u < 5) epi_unit(u, ev, p - 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            ev = acc;
+            acc = nxt;
+        }
+#pragma unroll
+        for (int u = 0; u < 5; ++u) epi_unit(u, ev, NP - 1);
+    }
+
     template <int l>
     static MPCD_DEV void layer(const WS<l> &w, char *lds, int wave, int lane)
     {
+#if MPCD_RW_ILV
+        hidden_ilv<l>(
+            [&](int j, int kc, int m, const u32x4 (&x)[3], f32x4 acc) { return mfma_bf(w.v[j][kc][wpl(m)], x[xpl(m)], acc); },
+            lds, wave, lane);
+#else
         hidden<l>([&](int j, int kc, const u32x4 (&x)[3], f32x4 acc) { return mfma_x3(w.v[j][kc], x, acc); }, lds, wave,
                   lane);
+#endif
     }
 
     template <int li>
     static MPCD_DEV void layer_res(const Res &r, const Tail &t, char *lds, int wave, int lane)
     {
+#if MPCD_RW_ILV
+        hidden_ilv<RES_L0 + li>(
+            [&](int j, int kc, int m, const u32x4 (&x)[3], f32x4 acc) {
+                const int g = (li * 2 + j) * 4 + kc;
+                if (g >= RES_AG) return mfma_bf(t.v[g - RES_AG][wpl(m)], x[xpl(m)], acc);
+                if (kc == 0 && m == 0) return mfma_agpr1<true>(r.a[g][wpl(m)], x[xpl(m)], acc);
+                return mfma_agpr1<false>(r.a[g][wpl(m)], x[xpl(m)], acc);
+            },
+            lds, wave, lane);
+#else
         hidden<RES_L0 + li>(
             [&](int j, int kc, const u32x4 (&x)[3], f32x4 acc) {
                 const int g = (li * 2 + j) * 4 + kc;
@@ -232,6 +340,7 @@ struct MlpRw {
                 return mfma_x3(t.v[g - RES_AG], x, acc);
             },
             lds, wave, lane);
+#endif
     }
 
     // x (4 features) -> fp32 row in XB and the three bf16 planes layer 0 reads

@@ -641,6 +641,7 @@ hipError_t launch_x3_d0(const MlpSampleArgs &a, int lay, hipStream_t stream)
 }  // namespace
 
 void mlp_x3_force_layout(int layout) { g_force_layout.store(layout); }
+int mlp_x3_layout_of(int64_t batch, int nb) { return mlp_x3_layout(batch, nb); }
 
 int mlp_packed_floats_x3(int d0)
 {

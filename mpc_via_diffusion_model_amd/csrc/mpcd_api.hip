@@ -74,6 +74,29 @@ int fail(int code, const char *fmt, ...)
         if (e_ != hipSuccess) return fail(MPCD_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
     } while (0)
 
+// Every entry point runs on its context's device and gives the caller's current device back on return
+// (a process driving several GPUs through torch keeps its own current device across our calls).
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        err = prev == dev ? hipSuccess : hipSetDevice(dev);
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
+#define DEVICE_GUARD(dev)                                                                                 \
+    DeviceGuard device_guard_(dev);                                                                       \
+    if (device_guard_.err != hipSuccess)                                                                  \
+    return fail(MPCD_EHIP, "hipSetDevice(%d): %s", (int)(dev), hipGetErrorString(device_guard_.err))
+
 struct PSpec {
     std::string name;
     std::vector<int64_t> shape;
@@ -493,7 +516,7 @@ int mpcd_create(int device, mpcd_ctx **out)
     int n = 0;
     HIP_TRY(hipGetDeviceCount(&n));
     if (device < 0 || device >= n) return fail(MPCD_EINVAL, "device %d of %d", device, n);
-    HIP_TRY(hipSetDevice(device));
+    DEVICE_GUARD(device);
     auto *c = new mpcd_ctx();
     c->device = device;
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
@@ -517,7 +540,7 @@ int mpcd_create(int device, mpcd_ctx **out)
 void mpcd_destroy(mpcd_ctx *c)
 {
     if (!c) return;
-    (void)hipSetDevice(c->device);
+    DeviceGuard device_guard_(c->device);
     for (DevBuf *b : {&c->params, &c->wpack, &c->wpack3, &c->cond_layers, &c->unet_pack, &c->plan, &c->tproj, &c->cproj, &c->flag,
                       &c->unet_ws, &c->step_ctx, &c->step_part, &c->step_out, &c->step_amax})
         b->release();
@@ -534,7 +557,7 @@ int mpcd_load_net(mpcd_ctx *c, const mpcd_net_desc *desc, const float *blob, siz
     if (!c || !blob) return fail(MPCD_EINVAL, "null argument");
     int rc = check_desc(desc);
     if (rc) return rc;
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
     c->net_loaded = false;
     c->plan_cached_valid = false;
     return upload_net(c, *desc, blob, n_floats);
@@ -575,7 +598,7 @@ int mpcd_sample(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr)
     if (cfg != (d.cfg_masked != 0)) return fail(MPCD_EINVAL, "CFG samplers need a cfg_masked net and vice versa");
     if (d.context_dim > 0 && !a->context) return fail(MPCD_EINVAL, "net has a context but none given");
     hipStream_t st = static_cast<hipStream_t>(stream_ptr);
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
 
     int rc = build_plan(c, a, c->plan_host);
     if (rc) return rc;
@@ -654,7 +677,8 @@ int mpcd_sample(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr)
         u.clamp_x0 = a->clamp_x0;
         u.wp1 = wp1;
         u.wf = wf;
-        size_t ws = unet_workspace_bytes(d, c->unet, a->sampler, a->batch, cfg ? 2 : 1);
+        u.fused = unet_use_fused(c->unet, u.mode);  // once: sizes the workspace and picks the kernels
+        size_t ws = unet_workspace_bytes(d, c->unet, u.fused, a->batch, cfg ? 2 : 1);
         if ((rc = c->unet_ws.ensure(ws))) return rc;
         u.workspace = c->unet_ws.p;
         rc = unet_sample(d, c->unet, u, st);
@@ -677,7 +701,7 @@ int mpcd_eps(mpcd_ctx *c, const float *x, int32_t t, const float *context, int32
     if (d.context_dim > 0 && !context) return fail(MPCD_EINVAL, "net has a context but none given");
     if (t < 0 || t >= c->n_steps) return fail(MPCD_EINVAL, "t out of range");
     hipStream_t st = static_cast<hipStream_t>(stream_ptr);
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
     StepPlan sp{};
     sp.t = t;
     c->plan_host.assign(1, sp);
@@ -713,7 +737,8 @@ int mpcd_eps(mpcd_ctx *c, const float *x, int32_t t, const float *context, int32
         u.x_in = x;
         u.eps_cond = eps_cond;
         u.eps_uncond = eps_uncond;
-        if ((rc = c->unet_ws.ensure(unet_workspace_bytes(d, c->unet, u.mode, batch, cfg ? 2 : 1)))) return rc;
+        u.fused = unet_use_fused(c->unet, u.mode);
+        if ((rc = c->unet_ws.ensure(unet_workspace_bytes(d, c->unet, u.fused, batch, cfg ? 2 : 1)))) return rc;
         u.workspace = c->unet_ws.p;
         rc = unet_sample(d, c->unet, u, st);
         if (rc) return fail(rc, "unet eps: %s", unet_last_error());
@@ -776,6 +801,15 @@ int mpcd_unet_form(mpcd_ctx *c, int32_t sampler, int32_t out[4])
     return MPCD_OK;
 }
 
+int mpcd_mlp_layout(int64_t batch, int32_t cfg_masked, int32_t *layout_out)
+{
+    if (batch < 1 || !layout_out) return fail(MPCD_EINVAL, "mpcd_mlp_layout: bad arguments");
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    *layout_out = mlp_x3_layout_of(batch, cfg_masked ? 2 : 1);
+    return MPCD_OK;
+}
+
 int mpcd_mlp_force_layout(int32_t layout)
 {
     if (layout < -1 || layout > 4)
@@ -805,7 +839,7 @@ int mpcd_debug_set(mpcd_ctx *c, float *dbg)
 int mpcd_clip_flag(mpcd_ctx *c, const float *x, int64_t n, int32_t *flag, void *stream_ptr)
 {
     if (!c || !x || !flag || n < 1) return fail(MPCD_EINVAL, "bad clip_flag arguments");
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
     HIP_TRY(launch_clip_flag(x, n, flag, c->sync_ws(), static_cast<hipStream_t>(stream_ptr)));
     return MPCD_OK;
 }
@@ -822,7 +856,7 @@ int mpcd_rollout_cost(mpcd_ctx *c, const mpcd_system_desc *sys, const double *x0
         return fail(MPCD_EINVAL, "calMPCCost needs n_u == 1 and H >= 3");
     if ((size_t)horizon * sys->n_u * 64 * sizeof(float) > 64 * 1024) return fail(MPCD_EUNSUP, "H*n_u too large");
     hipStream_t st = static_cast<hipStream_t>(stream_ptr);
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
     const int *flag = clip_flag;
     if (!flag) {
         HIP_TRY(launch_clip_flag(u_norm, batch * horizon * sys->n_u, c->flag.as<int>(), c->sync_ws(), st));
@@ -848,7 +882,7 @@ int mpcd_clip_flags(mpcd_ctx *c, const float *x, int64_t n_groups, int64_t group
 {
     if (!c || !x || !flags) return fail(MPCD_EINVAL, "null argument");
     if (n_groups < 1 || group_elems < 1) return fail(MPCD_EINVAL, "n_groups / group_elems");
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
     HIP_TRY(launch_clip_flags(x, n_groups, group_elems, flags, static_cast<hipStream_t>(stream_ptr)));
     return MPCD_OK;
 }
@@ -858,7 +892,7 @@ int mpcd_normalize_states(mpcd_ctx *c, const double *x, int64_t n_states, int32_
 {
     if (!c || !x || !mn || !mx || !out) return fail(MPCD_EINVAL, "null argument");
     if (n_states < 1 || dim < 1 || dim > 16) return fail(MPCD_EINVAL, "n_states / dim (1..16)");
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
     HIP_TRY(launch_normalize_states(x, n_states, dim, mn, mx, out, static_cast<hipStream_t>(stream_ptr)));
     return MPCD_OK;
 }
@@ -871,7 +905,7 @@ int mpcd_rollout_cost_grouped(mpcd_ctx *c, const mpcd_system_desc *sys, const do
     if (batch < 1 || horizon < 2 || group < 1 || batch % group) return fail(MPCD_EINVAL, "batch/group/horizon");
     int rc = check_system(sys, horizon);
     if (rc) return rc;
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
     HIP_TRY(launch_rollout_cost(*sys, nullptr, x0_dev, group, u_norm, umin, umax, flags, batch, horizon, cost,
                                 static_cast<hipStream_t>(stream_ptr)));
     return MPCD_OK;
@@ -888,7 +922,7 @@ int mpcd_control_step(mpcd_ctx *c, const mpcd_system_desc *sys, double *x, int64
     if (decimals > 15) return fail(MPCD_EINVAL, "decimals > 15");
     int rc = check_system(sys, horizon);
     if (rc) return rc;
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
     HIP_TRY(launch_control_step(*sys, x, n_states, group, u_norm, horizon, cost, umin, umax, flags, select_first,
                                 decimals, u_applied, best_index, best_cost, static_cast<hipStream_t>(stream_ptr)));
     return MPCD_OK;
@@ -900,7 +934,7 @@ int mpcd_unnormalize(mpcd_ctx *c, const float *x, int64_t n_rows, int32_t dim, c
     if (!c || !x || !mn || !mx || !out) return fail(MPCD_EINVAL, "null argument");
     if (dim < 1 || dim > 16 || n_rows < 1) return fail(MPCD_EINVAL, "dim must be 1..16");
     hipStream_t st = static_cast<hipStream_t>(stream_ptr);
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
     const int *flag = clip_flag;
     if (!flag) {
         HIP_TRY(launch_clip_flag(x, n_rows * dim, c->flag.as<int>(), c->sync_ws(), st));
@@ -914,7 +948,7 @@ int mpcd_argmin(mpcd_ctx *c, const double *cost, int64_t n, int64_t offset, mpcd
 {
     if (!c || !cost || !best || n < 1) return fail(MPCD_EINVAL, "bad argmin arguments");
     hipStream_t st = static_cast<hipStream_t>(stream_ptr);
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
     HIP_TRY(launch_argmin(cost, n, offset, best, st));
     return MPCD_OK;
 }
@@ -933,7 +967,7 @@ int mpcd_comm_init(mpcd_ctx *c, int32_t nranks, int32_t rank, const void *id_in)
 {
     if (!c || !id_in || nranks < 1 || rank < 0 || rank >= nranks) return fail(MPCD_EINVAL, "bad comm arguments");
     if (c->comm) return fail(MPCD_ESTATE, "communicator already initialised");
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
     std::string e;
     int rc = comm_create_rccl(nranks, rank, id_in, &c->comm, e);
     if (rc) return fail(rc, "%s", e.c_str());
@@ -946,7 +980,7 @@ int mpcd_comm_init_loopback(mpcd_ctx *c, int32_t nranks, int32_t rank, uint64_t 
 {
     if (!c || nranks < 1 || rank < 0 || rank >= nranks) return fail(MPCD_EINVAL, "bad comm arguments");
     if (c->comm) return fail(MPCD_ESTATE, "communicator already initialised");
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
     std::string e;
     int rc = comm_create_loopback(nranks, rank, group_key, &c->comm, e);
     if (rc) return fail(rc, "%s", e.c_str());
@@ -965,7 +999,7 @@ int mpcd_comm_info(mpcd_ctx *c, int32_t *nranks, int32_t *rank)
 
 static int comm_gather(mpcd_ctx *c, const void *send, void *recv, size_t count, size_t esz, hipStream_t st)
 {
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
     if (!c->comm) {  // single rank: the gather is a copy
         if (send != recv) HIP_TRY(hipMemcpyAsync(recv, send, count * esz, hipMemcpyDeviceToDevice, st));
         return MPCD_OK;
@@ -998,7 +1032,7 @@ int mpcd_allgather_f64(mpcd_ctx *c, const double *send, double *recv, size_t cou
 int mpcd_broadcast_f32(mpcd_ctx *c, float *buf, size_t count, int32_t root, void *stream)
 {
     if (!c || !buf || root < 0 || root >= c->nranks) return fail(MPCD_EINVAL, "bad broadcast arguments");
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
     if (!c->comm) return MPCD_OK;
     std::string e;
     int rc = c->comm->broadcast(buf, count * 4, root, static_cast<hipStream_t>(stream), e);
@@ -1008,7 +1042,7 @@ int mpcd_broadcast_f32(mpcd_ctx *c, float *buf, size_t count, int32_t root, void
 int mpcd_allreduce_max_i32(mpcd_ctx *c, int32_t *buf, size_t count, void *stream)
 {
     if (!c || !buf) return fail(MPCD_EINVAL, "null argument");
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
     return comm_reduce(c, buf, count, COMM_MAX_I32, static_cast<hipStream_t>(stream));
 }
 
@@ -1043,7 +1077,7 @@ int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, fl
     if (c->comm && !a->costs_all) return fail(MPCD_EINVAL, "costs_all is required with a communicator");
     if (a->clip_rule < MPCD_CLIP_CHAIN || a->clip_rule > MPCD_CLIP_NONE) return fail(MPCD_EINVAL, "clip_rule %d", a->clip_rule);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    HIP_TRY(hipSetDevice(c->device));
+    DEVICE_GUARD(c->device);
 
     // host staging (pinned): [context row | result block]
     // result block: {best, winner row [row] fp32, clip code int32} - one D2H copy
@@ -1299,7 +1333,7 @@ int mpcd_trainer_step(mpcd_trainer *tr, const float *x0, const float *context, c
 {
     if (!tr || !x0 || !context || !t || !noise || !context_mask || !loss || batch < 1)
         return fail(MPCD_EINVAL, "mpcd_trainer_step: null argument or empty batch");
-    HIP_TRY(hipSetDevice(tr->device));
+    DEVICE_GUARD(tr->device);
     TrainBatch b{x0, context, noise, context_mask, t, batch, hip_stream};
     std::string why;
     const int r = trainer_step(tr->t, b, update != 0, loss, &why);
@@ -1311,7 +1345,7 @@ int mpcd_trainer_step(mpcd_trainer *tr, const float *x0, const float *context, c
 int mpcd_trainer_params(mpcd_trainer *tr, int32_t which, float *host_out, size_t n_floats)
 {
     if (!tr || !host_out || which < 0 || which > 4) return fail(MPCD_EINVAL, "mpcd_trainer_params: bad argument");
-    HIP_TRY(hipSetDevice(tr->device));
+    DEVICE_GUARD(tr->device);
     const int r = trainer_read(tr->t, which, host_out, n_floats);
     if (r == -1) return fail(MPCD_EINVAL, "mpcd_trainer_params: %zu floats, the net has %lld", n_floats, (long long)tr->n_params);
     if (r != 0) return fail(MPCD_EHIP, "mpcd_trainer_params: copy failed");
@@ -1321,7 +1355,7 @@ int mpcd_trainer_params(mpcd_trainer *tr, int32_t which, float *host_out, size_t
 int mpcd_trainer_comm_init(mpcd_trainer *tr, int32_t nranks, int32_t rank, const void *id_in)
 {
     if (!tr || !id_in || nranks < 1 || rank < 0 || rank >= nranks) return fail(MPCD_EINVAL, "bad comm arguments");
-    HIP_TRY(hipSetDevice(tr->device));
+    DEVICE_GUARD(tr->device);
     std::string e;
     Comm *c = nullptr;
     if (int rc = comm_create_rccl(nranks, rank, id_in, &c, e)) return fail(rc, "%s", e.c_str());
@@ -1335,7 +1369,7 @@ int mpcd_trainer_comm_init(mpcd_trainer *tr, int32_t nranks, int32_t rank, const
 int mpcd_trainer_comm_init_loopback(mpcd_trainer *tr, int32_t nranks, int32_t rank, uint64_t group_key)
 {
     if (!tr || nranks < 1 || rank < 0 || rank >= nranks) return fail(MPCD_EINVAL, "bad comm arguments");
-    HIP_TRY(hipSetDevice(tr->device));
+    DEVICE_GUARD(tr->device);
     std::string e;
     Comm *c = nullptr;
     if (int rc = comm_create_loopback(nranks, rank, group_key, &c, e)) return fail(rc, "%s", e.c_str());
@@ -1349,7 +1383,7 @@ int mpcd_trainer_comm_init_loopback(mpcd_trainer *tr, int32_t nranks, int32_t ra
 void mpcd_trainer_destroy(mpcd_trainer *tr)
 {
     if (!tr) return;
-    (void)hipSetDevice(tr->device);
+    DeviceGuard device_guard_(tr->device);
     trainer_free(tr->t);
     delete tr;
 }

@@ -102,6 +102,7 @@ struct UnetSampleArgs {
     void *workspace;
     float *eps_cond, *eps_uncond;  // MODE_EPS / MODE_EPS1 outputs
     const float *x_in;             // MODE_EPS / MODE_EPS1 input
+    int32_t fused;                 // the form, decided once per call by unet_use_fused (it also sized workspace)
 };
 
 // epilogue kinds shared by both conv families
@@ -162,6 +163,9 @@ using TensorLookup = std::function<const float *(const char *)>;
 // Repacks conv weights into `pack` (device, grown as needed).
 int unet_prepare(const mpcd_net_desc &d, size_t n_tensors, const TensorLookup &dev, const TensorLookup &host,
                  UnetWeights &w, void *&pack, size_t &pack_bytes);
-size_t unet_workspace_bytes(const mpcd_net_desc &d, const UnetWeights &w, int mode, int64_t batch, int nb);
+// Whole-net (fused) or layer-by-layer form of one sample / eps call: read once per call (the process-wide
+// override may change between calls, from any thread) and passed to both the workspace sizing and the call.
+bool unet_use_fused(const UnetWeights &w, int mode);
+size_t unet_workspace_bytes(const mpcd_net_desc &d, const UnetWeights &w, bool fused, int64_t batch, int nb);
 int unet_sample(const mpcd_net_desc &d, const UnetWeights &w, const UnetSampleArgs &a, hipStream_t stream);
 const char *unet_last_error();

@@ -823,6 +823,8 @@ bool use_fused(const UnetWeights &W, int mode)
 
 void unet_force_path(int path) { g_unet_path.store(path); }
 
+bool unet_use_fused(const UnetWeights &W, int mode) { return use_fused(W, mode); }
+
 void unet_form(const UnetWeights &W, int mode, int32_t out[4])
 {
     const bool f = use_fused(W, mode);
@@ -832,12 +834,12 @@ void unet_form(const UnetWeights &W, int mode, int32_t out[4])
     out[3] = f ? unet_fused_waves_per_wg(*W.fused) : 0;
 }
 
-size_t unet_workspace_bytes(const mpcd_net_desc &d, const UnetWeights &W, int mode, int64_t batch, int nb)
+size_t unet_workspace_bytes(const mpcd_net_desc &d, const UnetWeights &W, bool fused, int64_t batch, int nb)
 {
     const Dims m = dims_of(d);
     // + the sampler state x [B][H][d] and the per-quad chain |x| maxima [B][H*d/4]
     const size_t state = sizeof(float) * ((size_t)batch * m.H * m.d + (size_t)batch * (m.H * m.d / 4 + 1));
-    if (use_fused(W, mode)) return state + 256 + unet_fused_scratch_bytes(*W.fused, batch);
+    if (fused) return state + 256 + unet_fused_scratch_bytes(*W.fused, batch);
     return sizeof(float) * ws_floats(m, batch * nb) + state;
 }
 
@@ -922,10 +924,13 @@ int sample_fused(const mpcd_net_desc &d, const UnetWeights &W, const UnetSampleA
 int unet_sample(const mpcd_net_desc &d, const UnetWeights &W, const UnetSampleArgs &a, hipStream_t st)
 {
     if (!W.ready) return uerr(MPCD_ESTATE, "UNet weights not prepared");
-    if (g_unet_path.load() == 2 && !use_fused(W, a.mode))
+    if (a.fused) {
+        if (!W.fused) return uerr(MPCD_EUNSUP, "fused U-Net form requested but not prepared: " + W.fused_why);
+        return sample_fused(d, W, a, st);
+    }
+    if (g_unet_path.load() == 2)  // forced fused, and unet_use_fused said no
         return uerr(MPCD_EUNSUP, "fused U-Net forced but not applicable: " +
                                      (W.fused ? std::string("sampler mode") : W.fused_why));
-    if (use_fused(W, a.mode)) return sample_fused(d, W, a, st);
     const Dims m = dims_of(d);
     const bool eps_mode = a.mode == MODE_EPS || a.mode == MODE_EPS1;
     const int nb = (a.mode == MODE_DDIM || a.mode == MODE_EPS1) ? 1 : 2;

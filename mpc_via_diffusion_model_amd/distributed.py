@@ -34,13 +34,19 @@ def shard(n_local, group=None):
     return rank * n_local, n_local * size
 
 
+def _staged(t, group):
+    """gloo moves host tensors only: device tensors of a gloo group go through a host copy."""
+    return t.cpu() if t.is_cuda and dist.get_backend(group) == "gloo" else t
+
+
 def gather_costs(cost_local, group=None):
     rank, size = world(group)
     if size == 1:
         return cost_local
-    out = torch.empty(size * cost_local.numel(), dtype=cost_local.dtype, device=cost_local.device)
-    dist.all_gather_into_tensor(out, cost_local.contiguous(), group=group)
-    return out
+    src = _staged(cost_local.contiguous(), group)
+    out = torch.empty(size * src.numel(), dtype=src.dtype, device=src.device)
+    dist.all_gather_into_tensor(out, src, group=group)
+    return out.to(cost_local.device)
 
 
 def argmin_nan_last(cost):
@@ -55,9 +61,9 @@ def broadcast_row(row_local, owner, group=None):
     rank, size = world(group)
     if size == 1:
         return row_local
-    buf = row_local.contiguous().clone()
+    buf = _staged(row_local.contiguous(), group).clone()
     dist.broadcast(buf, src=dist.get_global_rank(group, owner) if group is not None else owner, group=group)
-    return buf
+    return buf.to(row_local.device)
 
 
 def any_flag(flag_local, group=None):
@@ -66,9 +72,9 @@ def any_flag(flag_local, group=None):
     rank, size = world(group)
     if size == 1:
         return flag_local
-    t = flag_local.clone()
+    t = _staged(flag_local, group).clone()
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-    return t
+    return t.to(flag_local.device)
 
 
 def select(cost_local, rows_local, argmin, group=None):

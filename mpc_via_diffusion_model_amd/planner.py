@@ -326,6 +326,12 @@ class DiffusionMPC:
         return {"fused": bool(out[0]), "planes": int(out[1]), "rows_per_workgroup": int(out[2]),
                 "waves_per_workgroup": int(out[3])}
 
+    def mlp_layout(self, n_samples):
+        """The MLP sampler layout ("32x8", "16x8", "16x4", "rw32", "rw16") a sample call of n_samples runs."""
+        out = ctypes.c_int32()
+        N.check(self._lib.mpcd_mlp_layout(int(n_samples), int(self.spec.cfg), ctypes.byref(out)), "mpcd_mlp_layout")
+        return {v: k for k, v in MLP_LAYOUTS.items()}[out.value]
+
     def last_sample_ms(self):
         ms = ctypes.c_float()
         N.check(self._lib.mpcd_last_sample_ms(self._ctx, ctypes.byref(ms)), "mpcd_last_sample_ms")

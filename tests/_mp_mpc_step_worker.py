@@ -1,0 +1,50 @@
+"""Child process of tests/test_gpu_multiprocess.py (not collected by pytest): one rank of a world-size-N
+gloo group on cuda:0. Runs the composed mpc_step (comm=None: the exchange through torch.distributed over the
+gloo group, as a process per GPU would with RCCL) on its shard of the cfg2 candidates, then the NativeComm
+unique-id hand-off (mpcd_comm_unique_id on rank 0, broadcast over the group) without the RCCL init, which
+needs a GPU per rank. Writes its results to <out>.rank<r>.npz.
+
+    python tests/_mp_mpc_step_worker.py RANK WORLD PORT OUT B_TOTAL"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec, systems  # noqa: E402
+from mpc_via_diffusion_model_amd import _native as N  # noqa: E402
+from tests._util import make_mlp  # noqa: E402
+
+H, d, C, NSTEPS, SEED = 32, 2, 4, 100, 2
+
+
+def main():
+    rank, world, port, out, b_total = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], int(sys.argv[5])
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        net = make_mlp(d, H, C, seed=0)
+        plan = DiffusionMPC(NetSpec("mlp", state_dim=d, horizon=H, context_dim=C, dtype="f32x3"), net.state_dict(),
+                            variance_schedule="exponential", n_diffusion_steps=NSTEPS)
+        x0 = np.random.default_rng(1).uniform(-1, 1, C)
+        res = plan.mpc_step(x0, systems.get("double_int2d"), b_total // world, w=0.01, seed=SEED)
+        torch.cuda.synchronize()
+        # NativeComm's id plumbing (distributed.py NativeComm.__init__) up to, not including, mpcd_comm_init
+        uid = (ctypes.c_uint8 * N.MPCD_COMM_ID_BYTES)()
+        if rank == 0:
+            N.check(N.lib().mpcd_comm_unique_id(uid), "mpcd_comm_unique_id")
+        obj = [bytes(uid)]
+        dist.broadcast_object_list(obj, src=0)
+        np.savez(f"{out}.rank{rank}.npz", best_index=res.best_index, best_cost=res.best_cost, u_best=res.u_best,
+                 u0=res.u0, costs=res.costs.cpu().numpy(), uid=np.frombuffer(obj[0], dtype=np.uint8))
+    finally:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,4 +1,6 @@
 """Shared helpers for the parity tests (oracle side + tolerance checks)."""
+import os
+
 import numpy as np
 import torch
 
@@ -22,8 +24,11 @@ def make_unet(d, C, mults=(1, 2, 4), seed=0, cfg=True):
                              conditioning_embed_dim=C).eval()
 
 
-def assert_traj_close(got, ref, rel=REL_TRAJ, abs_elem=ABS_ELEM, what=""):
-    """per trajectory ||d||_2/||ref||_2 <= rel and elementwise |d| <= abs_elem*max(|ref|, 1)."""
+def assert_traj_close(got, ref, rel=REL_TRAJ, abs_elem=ABS_ELEM, what="", spread=None):
+    """per trajectory ||d||_2/||ref||_2 <= rel and elementwise |d| <= abs_elem*max(|ref|, 1).
+    spread: the oracle's own elementwise spread of an ill-conditioned chain (oracle_sensitivity); the elementwise
+    bar is then max(abs_elem, SPREAD_X * spread), and the measured error / spread ratio is appended to the file
+    $MPCD_SPREAD_LOG names (profiles/r4_spread_ratios.tsv is the GPU run's record)."""
     got = got.detach().cpu().double().numpy()
     ref = ref.detach().cpu().double().numpy()
     assert got.shape == ref.shape, (got.shape, ref.shape)
@@ -32,6 +37,12 @@ def assert_traj_close(got, ref, rel=REL_TRAJ, abs_elem=ABS_ELEM, what=""):
     r2 = ref.reshape(g2.shape)
     tr = np.linalg.norm(g2 - r2, axis=1) / np.maximum(np.linalg.norm(r2, axis=1), 1e-30)
     el = np.abs(got - ref) / np.maximum(np.abs(ref), 1.0)
+    if spread is not None:
+        abs_elem = max(abs_elem, SPREAD_X * spread)
+        log = os.environ.get("MPCD_SPREAD_LOG")
+        if log:
+            with open(log, "a") as f:
+                f.write(f"{what}\t{el.max():.4e}\t{spread:.4e}\t{el.max() / max(spread, 1e-30):.3f}\t{tr.max():.4e}\n")
     assert tr.max() <= rel, f"{what}: worst trajectory rel err {tr.max():.3e} (> {rel})"
     assert el.max() <= abs_elem, f"{what}: worst element err {el.max():.3e} (> {abs_elem})"
     return tr.max(), el.max()

@@ -10,7 +10,7 @@ from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec
 from oracle import sampler as osam
 from oracle import schedule as osch
 
-from ._util import SPREAD_X, assert_traj_close, make_unet, oracle_sensitivity
+from ._util import assert_traj_close, make_unet, oracle_sensitivity
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -116,7 +116,7 @@ def test_cfg_ddim_unet_pendulum_shape(dtype):
     ref, spread = oracle_sensitivity(lambda: osam.ddim_cfg(net, osch.buffers("exponential", N), ctx.expand(B, C), 0.01,
                                                            B, H, noise=noise, return_chain=True))
     got = plan.sample_trajectories(ctx, B, H, sample_fn="ddim_cfg", noise=noise, return_chain=True)
-    assert_traj_close(got[: ref.shape[0]], ref, abs_elem=max(1e-4, SPREAD_X * spread), what="unet ddim_cfg")
+    assert_traj_close(got[: ref.shape[0]], ref, spread=spread, what="unet ddim_cfg")
 
 
 def test_reference_ddim_temporal_unet():
@@ -130,7 +130,7 @@ def test_reference_ddim_temporal_unet():
     ref, spread = oracle_sensitivity(lambda: osam.ddim(net, osch.buffers("exponential", N), B, H, noise=noise,
                                                        return_chain=True))
     got = plan.sample_trajectories(None, B, H, sample_fn="ddim", noise=noise, return_chain=True)
-    assert_traj_close(got[: ref.shape[0]], ref, abs_elem=max(1e-4, SPREAD_X * spread), what="ddim TemporalUnet")
+    assert_traj_close(got[: ref.shape[0]], ref, spread=spread, what="ddim TemporalUnet")
 
 
 @pytest.mark.parametrize("dtype", FP32_KINDS)
@@ -249,4 +249,4 @@ def test_panda_trained_checkpoint_through_gpu(dtype, B):
         print(f"panda f16 trajectory rel err {rel:.3e}")
         assert torch.isfinite(got).all() and rel <= 5e-2
     else:
-        assert_traj_close(chain, ref, abs_elem=max(1e-4, SPREAD_X * spread), what=f"panda {dtype} B={B}")
+        assert_traj_close(chain, ref, spread=spread, what=f"panda {dtype} B={B}")

@@ -1,22 +1,25 @@
 """GPU parity of the U-Net kernels AT THE BENCH SIZES (BASELINE cfg 3 / 4 / 5 row counts).
 
 The conv tiling (rows per workgroup x register tile x persistent, and fused-or-not per residual block)
-is chosen by timing once per layer shape and row count, so the variants the bench runs are the ones
-picked at 32,768 / 131,072 / 262,144 rows. Here every candidate is forced in turn
-(mpcd_unet_force_tiling) at those row counts and must give the same bits (the K order and the GroupNorm
-summation order do not depend on the tiling), a slice of candidates is checked against the oracle forward,
-and one full-batch sampling run per config (Philox noise, replayed for the slice through
-mpcd_philox_noise) is checked against the oracle sampler (temporal_unet.py:287-358,
+is chosen by timing once per layer shape and row count, so the variants the layer-by-layer form runs are the
+ones picked at 32,768 / 131,072 / 262,144 rows. Here, with the layer-by-layer form forced
+(mpcd_unet_force_path: at these shapes the automatic choice is the whole-network fused launch), every
+candidate is forced in turn (mpcd_unet_force_tiling) at those row counts and must give the same bits (the K
+order and the GroupNorm summation order do not depend on the tiling); the fused form (what the bench runs)
+must give the same bits for any split of the rows, a ragged tail included; >= 256 candidates of both forms
+(the first and last 128: every row slot of a fused workgroup and the last workgroup) are checked against
+the oracle forward; and one full-batch sampling run per config (Philox noise, replayed for the same slice
+through mpcd_philox_noise) is checked against the oracle sampler (temporal_unet.py:287-358,
 diffusion_model_base.py:181-209)."""
 import numpy as np
 import pytest
 import torch
 
-from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec, force_unet_tiling, philox_noise
+from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec, force_unet_path, force_unet_tiling, philox_noise
 from oracle import sampler as osam
 from oracle import schedule as osch
 
-from ._util import SPREAD_X, assert_traj_close, make_unet, oracle_sensitivity
+from ._util import assert_traj_close, make_unet, oracle_sensitivity
 
 pytestmark = pytest.mark.gpu
 
@@ -28,8 +31,10 @@ CFGS = {"cfg3": (1, 32, 2, 16384, "f32x3", "exponential", 100),
         "cfg5": (4, 64, 12, 131072, "f16", "cosine", 250)}
 
 
-def _slice_idx(B):
-    return torch.tensor(sorted({0, 1, 17, B // 2 - 1, B // 2, B - 2, B - 1}))
+def _slice_idx(B, k=128):
+    """>= 256 candidates: the first and last k (every row slot of the fused workgroups - R / 2 = 1 or 2
+    candidates each - and the final workgroup) and a few in the middle."""
+    return torch.tensor(sorted(set(range(k)) | set(range(B - k, B)) | {B // 2 - 1, B // 2, (17 * 97) % B}))
 
 
 @pytest.mark.parametrize("name", sorted(CFGS))
@@ -43,8 +48,10 @@ def test_every_tiling_bit_identical_at_bench_rows(name):
     ctx = torch.rand(1, C, generator=g, device="cuda") * 2 - 1
     t = N // 3
     try:
+        force_unet_path("layered")
+        assert not plan.unet_form()["fused"], "layer-by-layer form not in force"
         force_unet_tiling(-1, -1)
-        ref_c, ref_u = plan.eps(x, t, ctx)  # the measured picks = what the bench runs
+        ref_c, ref_u = plan.eps(x, t, ctx)  # the measured layer-by-layer picks
         torch.cuda.synchronize()
         for i in range(MAX_CONV):
             force_unet_tiling(i, -2)
@@ -56,6 +63,14 @@ def test_every_tiling_bit_identical_at_bench_rows(name):
             assert torch.equal(ec, ref_c) and torch.equal(eu, ref_u), f"{name}: fused-block candidate {j} differs"
     finally:
         force_unet_tiling(-1, -1)
+        force_unet_path("auto")
+    # the whole-network form, as the bench runs it at this shape: the same bits for any split of the rows
+    assert plan.unet_form()["fused"], "fused form expected at the bench shape"
+    fc, fu = plan.eps(x, t, ctx)
+    h = B // 2 + 1
+    for lo, hi in ((0, h), (h, B), (1, B - 1)):
+        pc, pu = plan.eps(x[lo:hi].contiguous(), t, ctx)
+        assert torch.equal(pc, fc[lo:hi]) and torch.equal(pu, fu[lo:hi]), f"{name}: fused rows [{lo}, {hi}) differ"
     idx = _slice_idx(B)
     xs = x[idx.cuda()].cpu()
     k = idx.numel()
@@ -63,12 +78,13 @@ def test_every_tiling_bit_identical_at_bench_rows(name):
     with torch.no_grad():
         rc = net(xs, tt, ctx.cpu().expand(k, C), torch.zeros(k, 1))
         ru = net(xs, tt, ctx.cpu().expand(k, C), torch.ones(k, 1))
-    for got, ref, br in ((ref_c, rc, "cond"), (ref_u, ru, "uncond")):
-        got = got[idx.cuda()].cpu()
-        err = float((got - ref).abs().max())
-        scale = max(float(ref.abs().max()), 1.0)
-        assert err <= EPS_TOL[dtype] * scale, f"{name} {br}: eps err {err:.3e} vs oracle (scale {scale:.2f})"
-    assert torch.isfinite(ref_c).all() and torch.isfinite(ref_u).all()
+    for form, (gc, gu) in (("layered", (ref_c, ref_u)), ("fused", (fc, fu))):
+        for got, ref, br in ((gc, rc, "cond"), (gu, ru, "uncond")):
+            got = got[idx.cuda()].cpu()
+            err = float((got - ref).abs().max())
+            scale = max(float(ref.abs().max()), 1.0)
+            assert err <= EPS_TOL[dtype] * scale, f"{name} {form} {br}: eps err {err:.3e} vs oracle (scale {scale:.2f})"
+        assert torch.isfinite(gc).all() and torch.isfinite(gu).all()
 
 
 @pytest.mark.parametrize("name", sorted(CFGS))
@@ -106,7 +122,7 @@ def test_full_batch_sampling_slice_matches_oracle(name):
         print(f"{name} f16 full-batch slice trajectory rel err {rel:.3e}")
         assert rel <= 5e-2
     else:
-        assert_traj_close(g, ref, abs_elem=max(1e-4, SPREAD_X * spread), what=f"{name} full batch")
+        assert_traj_close(g, ref, spread=spread, what=f"{name} full batch")
         # chain |x| maxima (the chain-wide clip test's input) for the slice
         ref_am = ref_chain.abs().amax(dim=(0, 2, 3))
         assert torch.allclose(am[idx.cuda()].cpu(), ref_am, rtol=1e-4, atol=1e-4)

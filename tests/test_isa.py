@@ -56,6 +56,25 @@ def test_every_kernel_keeps_packed_reads_of_transcendentals_two_wait_states_away
         "the fused U-Net's packed Mish should read exp / rcp results (pattern not found: scan broken?)"
 
 
+def test_every_mfma_source_two_wait_states_after_a_valu_write(tmp_path):
+    """csrc/mlp_rw.hip issues MFMAs with AGPR weight operands as inline asm, which the compiler's hazard pass does
+    not treat as MFMAs: no MFMA of the library may read a register a VALU op wrote under 2 wait states before."""
+    import mfma_hazard as mh
+    lines = _disassemble(tmp_path)
+    assert any("mlp_rw_kernel" in ln for ln in lines), "mlp_rw_kernel not found in the code object"
+    assert any("v_mfma" in ln and ", a[" in ln for ln in lines), "no MFMA with AGPR operands (resident weights?)"
+    bad = mh.scan(lines)
+    assert not bad, f"{len(bad)} MFMA sources written by a VALU op under 2 wait states: {bad[:3]}"
+
+
+def test_mfma_scan_finds_a_close_valu_write():
+    import mfma_hazard as mh
+    asm = ["_Z1kv:", "  v_mov_b32_e32 v31, v33", "  v_mfma_f32_16x16x32_bf16 v[28:31], a[20:23], v[0:3], v[28:31]",
+           "  v_mov_b32_e32 v2, v33", "  s_nop 1", "  v_mfma_f32_16x16x32_bf16 v[28:31], a[20:23], v[0:3], v[28:31]",
+           "  v_mov_b32_e32 v40, v33", "  v_mfma_f32_16x16x32_bf16 v[28:31], a[20:23], v[0:3], v[28:31]"]
+    assert [(b[2].split()[1], b[3]) for b in mh.scan(asm)] == [("v31,", 0), ("v2,", 2)][:1]
+
+
 def test_scan_finds_the_one_wait_state_pattern():
     import trans_hazard as th
     asm = ["_Z1kv:", "  v_rcp_f32_e32 v25, v25", "  s_nop 0", "  v_pk_fma_f32 v[24:25], v[24:25], -2.0, 1.0",
