@@ -46,7 +46,8 @@ MPCD_DEV f32x4 mfma_x3_agpr(const u32x4 &w0, const u32x4 &w1, const u32x4 &w2, c
         "v_mfma_f32_16x16x32_bf16 %0, %1, %6, %0\n\t"   // w0 x2
         "v_mfma_f32_16x16x32_bf16 %0, %2, %4, %0\n\t"   // w1 x0
         "v_mfma_f32_16x16x32_bf16 %0, %1, %5, %0\n\t"   // w0 x1
-        "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0"       // w0 x0
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0\n\t"  // w0 x0
+        "s_nop 7"                                        // result -> VALU read (see mfma_agpr1)
         : "+v"(acc)
         : "a"(w0), "a"(w1), "a"(w2), "v"(x[0]), "v"(x[1]), "v"(x[2]));
     return acc;
@@ -56,15 +57,21 @@ MPCD_DEV f32x4 mfma_x3_agpr(const u32x4 &w0, const u32x4 &w1, const u32x4 &w2, c
 constexpr int wpl(int m) { return m == 0 ? 2 : (m == 1 || m == 3) ? 1 : 0; }
 constexpr int xpl(int m) { return (m == 0 || m == 3 || m == 5) ? 0 : (m == 1 || m == 4) ? 1 : 2; }
 
-// One partial product with the weight plane in an AGPR. NOP: the first MFMA of a chain, whose accumulator may
-// have just been written by a VALU op (2 wait states); inside a chain the accumulator comes from the previous
-// MFMA (srcC forwarding, no wait). tests/test_isa.py checks every MFMA source of the library for a VALU write
-// under 2 wait states.
-template <bool NOP>
+// One partial product with the weight plane in an AGPR. The compiler's hazard pass does not see an MFMA in an
+// asm statement, so its waits are written here: FIRST (the chain's first product), 2 wait states for a VALU
+// write of the accumulator just before; LAST (the chain's last product), 8 wait states after it, before any
+// VALU op may read the result (what hipcc inserts after the builtin v_mfma_f32_16x16x32_bf16 on gfx950).
+// Inside a chain the accumulator goes MFMA to MFMA (srcC forwarding, no wait). tests/test_isa.py checks both
+// rules on every MFMA of the library.
+template <bool FIRST, bool LAST>
 MPCD_DEV f32x4 mfma_agpr1(const u32x4 &w, const u32x4 &x, f32x4 acc)
 {
-    if constexpr (NOP)
+    if constexpr (FIRST && LAST)
+        asm("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\ts_nop 7" : "+v"(acc) : "a"(w), "v"(x));
+    else if constexpr (FIRST)
         asm("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(x));
+    else if constexpr (LAST)
+        asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\ts_nop 7" : "+v"(acc) : "a"(w), "v"(x));
     else
         asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(x));
     return acc;
@@ -129,6 +136,24 @@ struct MlpRw {
         }
     }
 
+    // fragment f (= (j * KC + kc) * 3 + plane) of layer l for this wave: load_ws one piece at a time, issued in
+    // the free MFMA slots of an earlier layer (hidden_ilv's side work)
+    template <int l>
+    static MPCD_DEV void load_ws1(WS<l> &w, const float *__restrict__ wp, int wave, int lane16, int f)
+    {
+        constexpr int K = A::K[l], N = A::N[l], KC = K / 32, NT = N / 16;
+        const uint64_t a = (uint64_t)(wp + woffx<D0>(l));
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(3 * K * N * 2), 0x00020000);
+        const int j = f / (KC * 3), kc = (f / 3) % KC, pl = f % 3;
+        const int nt = min(nt_of<l>(wave, j), NT - 1);
+        const int soff = __builtin_amdgcn_readfirstlane(((nt * KC + kc) * 3 + pl) * 1024);
+        w.v[j][kc][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
+    }
+    template <int l>
+    static constexpr int NFRAG = TL<l> * (A::K[l] / 32) * 3;
+
     // Resident fragments: group g = ((li * 2 + j) * 4 + kc), planes 0..2 (AGPRs); Tail: groups RES_AG.. of
     // layer 7, streamed like the other layers (VGPRs)
     struct Res {
@@ -137,6 +162,16 @@ struct MlpRw {
     struct Tail {
         u32x4 v[RES_G - RES_AG][3];
     };
+    static MPCD_DEV void load_tail1(Tail &t, const float *__restrict__ wp, int wave, int lane16, int f)
+    {
+        const uint64_t a = (uint64_t)(wp + woffx<D0>(RES_L0 + RES_NL - 1));
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(3 * 128 * 128 * 2), 0x00020000);
+        const int g = RES_AG + f / 3, pl = f % 3, j = (g / 4) & 1, kc = g & 3, nt = wave + 4 * j;
+        const int soff = __builtin_amdgcn_readfirstlane(((nt * 4 + kc) * 3 + pl) * 1024);
+        t.v[g - RES_AG][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
+    }
     static MPCD_DEV void load_tail(Tail &t, const float *__restrict__ wp, int wave, int lane16)
     {
         const uint64_t a = (uint64_t)(wp + woffx<D0>(RES_L0 + RES_NL - 1));
@@ -243,8 +278,14 @@ struct MlpRw {
 
     // Pipelined form of hidden(). MM1(j, kc, m, x[3], acc) -> acc: partial product m (0..5, smallest first:
     // the mfma_x3 order) of k-chunk kc of n-tile j. Same products in the same order as hidden(): bit-identical.
-    template <int l, class MM1>
-    static MPCD_DEV void hidden_ilv(MM1 mm1, char *lds, int wave, int lane)
+    // free MFMA slots of layer l's pipeline (the first 5 of every pass but the first carry epilogue units)
+    template <int l>
+    static constexpr int FREE = TL<l> * CL<l> * (A::K[l] / 32) * 6 - 5 * (TL<l> * CL<l> - 1);
+
+    // SIDE(k), k < NS: side work, one item per free slot in order; items beyond the free slots (and all of them
+    // on a wave with no tile) run after the layer's MFMAs
+    template <int l, int NS, class MM1, class SIDE>
+    static MPCD_DEV void hidden_ilv(MM1 mm1, SIDE side, char *lds, int wave, int lane)
     {
         constexpr int K = A::K[l], N = A::N[l], KC = K / 32, NT = N / 16, T = TL<l>, NC = CL<l>, EPI = epi_of(l);
         constexpr int NP = T * NC, NI = NP * KC;  // passes; (pass, k-chunk) steps
@@ -252,7 +293,11 @@ struct MlpRw {
         constexpr bool in_shared = l == 0 && NB == 2;  // CFG: both branches read the candidate's x
         static_assert(T == 1 || NT % 4 == 0, "only a one-tile layer can leave a wave idle");
         if constexpr (NT < 4 && !SPL<l>)
-            if (wave >= NT) return;  // N = 32 at 16 rows: waves 2, 3 have no tile
+            if (wave >= NT) {  // N = 32 at 16 rows: waves 2, 3 have no tile
+#pragma unroll
+                for (int k = 0; k < NS; ++k) side(k);
+                return;
+            }
         auto jp = [](int p) { return p / NC; };
         auto cp = [](int p) { return p % NC; };
         auto init_of = [&](int p) {
@@ -297,6 +342,7 @@ struct MlpRw {
                     acc = mm1(jp(p), kc, m, xb[i % 3], acc);
                     const int u = kc * 6 + m;
                     if (p > 0 && u < 5) epi_unit(u, ev, p - 1);
+                    else if (i * 6 + m - 5 * p < NS) side(i * 6 + m - 5 * p);  // the k-th free slot
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
@@ -305,33 +351,43 @@ struct MlpRw {
         }
 #pragma unroll
         for (int u = 0; u < 5; ++u) epi_unit(u, ev, NP - 1);
+#pragma unroll
+        for (int k = FREE<l>; k < NS; ++k) side(k);
     }
 
-    template <int l>
-    static MPCD_DEV void layer(const WS<l> &w, char *lds, int wave, int lane)
+    template <int l, int NS = 0, class SIDE>
+    static MPCD_DEV void layer(const WS<l> &w, SIDE side, char *lds, int wave, int lane)
     {
 #if MPCD_RW_ILV
-        hidden_ilv<l>(
+        hidden_ilv<l, NS>(
             [&](int j, int kc, int m, const u32x4 (&x)[3], f32x4 acc) { return mfma_bf(w.v[j][kc][wpl(m)], x[xpl(m)], acc); },
-            lds, wave, lane);
+            side, lds, wave, lane);
 #else
         hidden<l>([&](int j, int kc, const u32x4 (&x)[3], f32x4 acc) { return mfma_x3(w.v[j][kc], x, acc); }, lds, wave,
                   lane);
+#pragma unroll
+        for (int k = 0; k < NS; ++k) side(k);
 #endif
     }
 
-    template <int li>
-    static MPCD_DEV void layer_res(const Res &r, const Tail &t, char *lds, int wave, int lane)
+    template <int li, int NS = 0, class SIDE>
+    static MPCD_DEV void layer_res(const Res &r, const Tail &t, SIDE side, char *lds, int wave, int lane)
     {
 #if MPCD_RW_ILV
-        hidden_ilv<RES_L0 + li>(
+        hidden_ilv<RES_L0 + li, NS>(
             [&](int j, int kc, int m, const u32x4 (&x)[3], f32x4 acc) {
                 const int g = (li * 2 + j) * 4 + kc;
                 if (g >= RES_AG) return mfma_bf(t.v[g - RES_AG][wpl(m)], x[xpl(m)], acc);
-                if (kc == 0 && m == 0) return mfma_agpr1<true>(r.a[g][wpl(m)], x[xpl(m)], acc);
-                return mfma_agpr1<false>(r.a[g][wpl(m)], x[xpl(m)], acc);
+                const bool first = kc == 0 && m == 0;
+                // LAST: the pass's last product, or the one before the VGPR-tail groups (a builtin MFMA then
+                // reads the result: srcC forwarding needs no wait, but the compiler may copy it between)
+                const bool last = (kc == 3 || g + 1 == RES_AG) && m == 5;
+                if (first && last) return mfma_agpr1<true, true>(r.a[g][wpl(m)], x[xpl(m)], acc);
+                if (first) return mfma_agpr1<true, false>(r.a[g][wpl(m)], x[xpl(m)], acc);
+                if (last) return mfma_agpr1<false, true>(r.a[g][wpl(m)], x[xpl(m)], acc);
+                return mfma_agpr1<false, false>(r.a[g][wpl(m)], x[xpl(m)], acc);
             },
-            lds, wave, lane);
+            side, lds, wave, lane);
 #else
         hidden<RES_L0 + li>(
             [&](int j, int kc, const u32x4 (&x)[3], f32x4 acc) {
@@ -340,6 +396,8 @@ struct MlpRw {
                 return mfma_x3(t.v[g - RES_AG], x, acc);
             },
             lds, wave, lane);
+#pragma unroll
+        for (int k = 0; k < NS; ++k) side(k);
 #endif
     }
 
@@ -515,67 +573,91 @@ struct MlpRw {
         f32x4 nz[NZT][NB];
         StepPlan sp = load_plan(p.plan, 0);
         fetch_noise(nz, p, sp, 0, cand0, wave, lane);
-        const int tpi = threadIdx.x < COND_TOTAL / 4 ? (int)threadIdx.x : 0;
+        const int tpi = threadIdx.x < COND_TOTAL / 4 ? (int)threadIdx.x : threadIdx.x < COND_TOTAL / 2 ? (int)threadIdx.x - COND_TOTAL / 4 : 0;
         f32x4 tpre = reinterpret_cast<const f32x4 *>(p.tproj)[tpi];
+#ifdef MPCD_PROF_LAYERS
+        // experiment build only: per-wave shader-clock cycles of each segment (work, then barrier wait), the
+        // dump format of mlp_x3.hip (tools/layer_prof.py)
+        uint64_t tacc[2 * 16] = {};
+        const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+        uint64_t tprev = __builtin_readcyclecounter();
+        const uint64_t ct0 = tprev;
+        int bk = 0;
+        auto bar = [&] {
+            uint64_t t = __builtin_readcyclecounter();
+            tacc[2 * bk] += t - tprev;
+            lds_barrier();
+            tprev = __builtin_readcyclecounter();
+            tacc[2 * bk + 1] += tprev - t;
+            bk = bk == 13 ? 0 : bk + 1;
+        };
+#else
         auto bar = [] { lds_barrier(); };
+#endif
 
         for (int s = 0; s < p.n_steps; ++s) {
             // launder the weight base: stops LICM hoisting the streamed layers' loads out of the loop
             asm volatile("" : "+s"(wofs), "+v"(lane16));
             const float *ws = wp + wofs;
+            auto none = [](int) {};
+            // Each layer's fragments are issued one at a time in the free MFMA slots of an earlier layer
+            // (hidden_ilv side work): the vector-memory issue rides under MFMAs instead of stalling a layer, and
+            // the register budget (one wave per SIMD, 512 registers, 252 AGPRs of resident weights) holds: L8's
+            // 96 registers are in flight from L5 on, everything else one or two layers ahead.
             WS<1> w1;
             load_ws<1>(w1, ws, wave, lane16);
             WS<2> w2;
             load_ws<2>(w2, ws, wave, lane16);
             bar();
-            // this step's time projections + cond biases (+ shared context part) -> TPU / TPC
-            if (threadIdx.x < COND_TOTAL / 4) {
-                const f32x4 u = tpre + reinterpret_cast<const f32x4 *>(lds + L::BIC)[tpi];
-                reinterpret_cast<f32x4 *>(lds + L::TPU)[tpi] = u;
-                reinterpret_cast<f32x4 *>(lds + L::TPC)[tpi] = u + reinterpret_cast<const f32x4 *>(lds + L::CPS)[tpi];
+            // this step's time projections + cond biases (+ shared context part) -> TPU / TPC: one f32x4 per thread
+            if (threadIdx.x < COND_TOTAL / 2) {
+                const bool ctx_half = threadIdx.x >= COND_TOTAL / 4;
+                const int k = ctx_half ? (int)threadIdx.x - COND_TOTAL / 4 : (int)threadIdx.x;
+                f32x4 u = tpre + reinterpret_cast<const f32x4 *>(lds + L::BIC)[k];
+                if (ctx_half) u = u + reinterpret_cast<const f32x4 *>(lds + L::CPS)[k];
+                reinterpret_cast<f32x4 *>(lds + (ctx_half ? L::TPC : L::TPU))[k] = u;
             }
             tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 1 < p.n_steps ? s + 1 : s) * COND_TOTAL)[tpi];
-            layer<0>(w0, lds, wave, lane);
             WS<3> w3;
-            load_ws<3>(w3, ws, wave, lane16);
+            layer<0, NFRAG<3>>(w0, [&](int k) { load_ws1<3>(w3, ws, wave, lane16, k); }, lds, wave, lane);
             bar();
-            layer<1>(w1, lds, wave, lane);
             WS<4> w4;
-            load_ws<4>(w4, ws, wave, lane16);
+            layer<1, NFRAG<4>>(w1, [&](int k) { load_ws1<4>(w4, ws, wave, lane16, k); }, lds, wave, lane);
             bar();
-            layer<2>(w2, lds, wave, lane);
+            layer<2>(w2, none, lds, wave, lane);
             bar();
-            layer<3>(w3, lds, wave, lane);
+            layer<3>(w3, none, lds, wave, lane);
             bar();
-            layer<4>(w4, lds, wave, lane);
+            layer<4>(w4, none, lds, wave, lane);
             bar();
-            Tail tail;
-            layer_res<0>(res, tail, lds, wave, lane);
-            // register budget (one wave per SIMD, 512 registers, 252 AGPRs hold resident weights): each layer's
-            // fragments are issued as late as the L2 latency allows - L8's 96 registers two layers ahead
             WS<8> w8;
-            load_ws<8>(w8, ws, wave, lane16);
+            Tail tail;
+            layer_res<0>(res, tail, none, lds, wave, lane);
             bar();
-            layer_res<1>(res, tail, lds, wave, lane);
+            layer_res<1, NFRAG<8>>(res, tail, [&](int k) { load_ws1<8>(w8, ws, wave, lane16, k); }, lds, wave, lane);
             load_tail(tail, ws, wave, lane16);
             bar();
-            layer_res<2>(res, tail, lds, wave, lane);
             WS<9> w9;
+            layer_res<2>(res, tail, none, lds, wave, lane);
             load_ws<9>(w9, ws, wave, lane16);
             bar();
-            layer<8>(w8, lds, wave, lane);
             WS<10> w10;
-            load_ws<10>(w10, ws, wave, lane16);
+            layer<8>(w8, none, lds, wave, lane);
+            load_ws<10>(w10, ws, wave, lane16);  // after L8: w8's 96 registers are free again
             bar();
-            layer<9>(w9, lds, wave, lane);
             WS<11> w11;
-            load_ws<11>(w11, ws, wave, lane16);
             WS<12> w12;
-            load_ws<12>(w12, ws, wave, lane16);
             WS<13> w13;
-            load_ws<13>(w13, ws, wave, lane16);
+            layer<9, NFRAG<11> + NFRAG<12> + NFRAG<13>>(
+                w9,
+                [&](int k) {
+                    if (k < NFRAG<11>) load_ws1<11>(w11, ws, wave, lane16, k);
+                    else if (k < NFRAG<11> + NFRAG<12>) load_ws1<12>(w12, ws, wave, lane16, k - NFRAG<11>);
+                    else load_ws1<13>(w13, ws, wave, lane16, k - NFRAG<11> - NFRAG<12>);
+                },
+                lds, wave, lane);
             bar();
-            layer<10>(w10, lds, wave, lane);
+            layer<10>(w10, none, lds, wave, lane);
             const StepPlan cur = sp;
             f32x4 nzc[NZT][NB];
 #pragma unroll
@@ -588,12 +670,28 @@ struct MlpRw {
             }
             load_ws<0>(w0, ws, wave, lane16);  // next step's layer 0 (unconditional: path-independent load count)
             bar();
-            layer<11>(w11, lds, wave, lane);
+            layer<11>(w11, none, lds, wave, lane);
             bar();
-            layer<12>(w12, lds, wave, lane);
+            layer<12>(w12, none, lds, wave, lane);
             bar();
             final_and_update(w13, lds, p, cur, s, cand0, nzc, am, wave, lane);
         }
+#ifdef MPCD_PROF_LAYERS
+        {
+            const uint64_t t = __builtin_readcyclecounter();
+            tacc[2 * 15] += t - tprev;
+            if (p.dbg && blockIdx.x < 32 / RW_W && lane == 0)  // 32 wave slots
+                for (int i = 0; i < 32; ++i) p.dbg[(blockIdx.x * RW_W + (threadIdx.x >> 6)) * 32 + i] = (float)tacc[i];
+            if (p.dbg && threadIdx.x == 0) {  // per-block loop start / end (memrealtime, low 32 bits)
+                p.dbg[4096 + blockIdx.x * 2] = __builtin_bit_cast(float, (uint32_t)rt0);
+                p.dbg[4096 + blockIdx.x * 2 + 1] = __builtin_bit_cast(float, (uint32_t)__builtin_amdgcn_s_memrealtime());
+            }
+            if (p.dbg && blockIdx.x < 8 && threadIdx.x == 0) {  // shader clock = d(memtime) / d(memrealtime) x 100 MHz
+                p.dbg[8 * 4 * 32 + blockIdx.x * 2] = (float)(t - ct0);
+                p.dbg[8 * 4 * 32 + blockIdx.x * 2 + 1] = (float)(__builtin_amdgcn_s_memrealtime() - rt0);
+            }
+        }
+#endif
         if (SMODE != MODE_EPS && SMODE != MODE_EPS1 && p.chain_absmax) {
             const int col = lane & 15;
             store_chain_absmax<CPW, RW_T>(reinterpret_cast<uint32_t *>(lds + L::AMX), am, col,

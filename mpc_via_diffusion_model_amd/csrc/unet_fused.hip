@@ -270,6 +270,7 @@ struct FArgs {
     uint32_t *amq;
     float *eps_c, *eps_u;  // MODE_EPS outputs
     char *scratch;         // skip spill: [row][L][C], fp16 (P = 1) or fp32 (P = 3)
+    int64_t nblk;          // row blocks of R rows; workgroup b runs blocks b, b + gridDim.x, ... (persistent grid)
     uint64_t *prof;        // diagnostics (MPCD_FUSED_PROF) or null: per workgroup < kProfWgs and op, wave 0's
                            // s_memtime at op start / GEMM done / statistics done / op done
 };
@@ -360,11 +361,27 @@ MPCD_DEV f32x2 hi2(const f32x4 &v) { return f32x2{v[2], v[3]}; }
 constexpr float kLog2e = 1.44269504088896341f, kLn2 = 0.693147180559945309f;
 // Mish of a pair given in log2 units (z = y log2 e): y (1 - 2 / (n (n + 2) + 2)), n = e^y (common.h mish); four
 // transcendentals, four packed ops
+// The two transcendentals of a pair are issued together, followed by 2 wait states, so the packed op that reads
+// them is never closer (packed reads of a v_exp / v_rcp result one wait state behind it gave wrong results on
+// gfx950: profiles/r3_hazard_ab.txt; the compiler's scheduler alone kept that distance only by chance, and a new
+// instantiation lost it). Same instructions as __builtin_amdgcn_exp2f / rcpf: the same bits.
+MPCD_DEV f32x2 exp2_pair(f32x2 z)
+{
+    float a, b;
+    asm("v_exp_f32 %0, %2\n\tv_exp_f32 %1, %3\n\ts_nop 1" : "=&v"(a), "=&v"(b) : "v"(z[0]), "v"(z[1]));
+    return f32x2{a, b};
+}
+MPCD_DEV f32x2 rcp_pair(f32x2 x)
+{
+    float a, b;
+    asm("v_rcp_f32 %0, %2\n\tv_rcp_f32 %1, %3\n\ts_nop 1" : "=&v"(a), "=&v"(b) : "v"(x[0]), "v"(x[1]));
+    return f32x2{a, b};
+}
 MPCD_DEV f32x2 mish2_log2(f32x2 z)
 {
-    const f32x2 n = {__builtin_amdgcn_exp2f(z[0]), __builtin_amdgcn_exp2f(z[1])};
+    const f32x2 n = exp2_pair(z);
     const f32x2 den = fma2(n, n + 2.0f, f32x2{2.0f, 2.0f});
-    const f32x2 r = {__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
+    const f32x2 r = rcp_pair(den);
     return z * fma2(r, f32x2{-2.0f * kLn2, -2.0f * kLn2}, f32x2{kLn2, kLn2});
 }
 
@@ -906,7 +923,7 @@ MPCD_DEV void run_ops(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
     }
 }
 
-template <int P, int R, int H, int W>
+template <int P, int R, int H, int W, bool PERS>
 __global__ __launch_bounds__(64 * W) void unet_fused_kernel(const FArgs a)
 {
     constexpr int FT = 64 * W;
@@ -915,9 +932,13 @@ __global__ __launch_bounds__(64 * W) void unet_fused_kernel(const FArgs a)
     static_assert(pg.ok, "fused U-Net program does not fit this (P, R, H)");
     constexpr int RC = R / 2, PLB = pg.plb;
     const int tid = threadIdx.x;
-    const int64_t cand0 = (int64_t)blockIdx.x * RC, row0 = (int64_t)blockIdx.x * R;
     const int d = a.d;
     APre<P> pre;
+    // Row blocks blockIdx.x, + gridDim.x, ...: a grid of one block per row block runs one iteration; a persistent
+    // grid (MPCD_FUSED_PERSIST) keeps each CU's workgroups walking the net together, block after block, so the
+    // weights of the ops in flight stay in the XCD's L2 instead of every late-starting workgroup re-fetching them.
+    for (int64_t blk = blockIdx.x; blk < a.nblk; blk += gridDim.x) {
+    const int64_t cand0 = blk * RC, row0 = blk * R;
     // the first conv's weights are in flight while x is staged
     prefetch_op<P, R, H, W, 0>(a, __builtin_amdgcn_readfirstlane(tid >> 6), tid & 63, pre);
 
@@ -972,6 +993,9 @@ __global__ __launch_bounds__(64 * W) void unet_fused_kernel(const FArgs a)
         if (a.chain) *reinterpret_cast<f32x4 *>(a.chain + (size_t)(a.s + 1) * a.batch * flat + off) = o;
         if (a.last && a.x_out != a.x) *reinterpret_cast<f32x4 *>(a.x_out + off) = o;
     }
+    if constexpr (!PERS) break;  // one block per workgroup: no loop-carried state (the registers of round 3)
+    lds_barrier();  // E (region Z) is read above; the next block stages x into region Z
+    }
 }
 
 // ---- host
@@ -984,7 +1008,7 @@ struct Cfg {
 // (1, 2, 64, 4): two or three 4-wave workgroups per CU, their barriers independent (cfg5 14.7 ms per CFG evaluation
 // vs 15.3 for one 8-wave workgroup of 4 rows); the split-bf16 nets keep 4-row blocks (their weights, three planes,
 // miss the L2 per block: cfg3 3.98 ms with 2-row blocks vs 3.58)
-#define MPCD_FUSED_CFGS C_(1, 2, 64, 4) C_(3, 4, 32, 8) C_(1, 8, 32, 8) C_(3, 2, 64, 8) C_(1, 4, 64, 8) \
+#define MPCD_FUSED_CFGS C_(1, 2, 64, 4) C_(3, 4, 32, 8) C_(1, 8, 32, 8) C_(3, 2, 64, 8) C_(1, 2, 128, 8) C_(1, 4, 64, 8) \
     C_(1, 2, 64, 8) C_(3, 2, 32, 4)
 constexpr Cfg kCfgs[] = {
 #define C_(p, r, h, w) {p, r, h, w},
@@ -1001,14 +1025,39 @@ const Prog *prog_of(int P, int R, int H, int W)
     return nullptr;
 }
 
+// MPCD_FUSED_PERSIST=1: a grid of (resident workgroups per CU) x CUs walking the row blocks (experiment switch)
+bool fused_persistent()
+{
+    static const bool on = [] {
+        const char *e = getenv("MPCD_FUSED_PERSIST");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 template <int P, int R, int H, int W>
 hipError_t launch_cfg(const FArgs &fa, unsigned grid, hipStream_t st)
 {
-    constexpr auto kfn = &unet_fused_kernel<P, R, H, W>;
-    if (hipError_t e = allow_max_lds<kfn>(); e != hipSuccess) return e;
     constexpr size_t lds = ProgOf<P, R, H, W>::v.lds;
-    hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * W), lds, st, fa);
-    return hipGetLastError();
+    if (P == 1 || !fused_persistent()) {  // (f16 weights, 2 MB, stay L2-resident: no persistent form)
+        constexpr auto kfn = &unet_fused_kernel<P, R, H, W, false>;
+        if (hipError_t e = allow_max_lds<kfn>(); e != hipSuccess) return e;
+        hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * W), lds, st, fa);
+        return hipGetLastError();
+    }
+    if constexpr (P != 1) {
+        constexpr auto kfn = &unet_fused_kernel<P, R, H, W, true>;
+        if (hipError_t e = allow_max_lds<kfn>(); e != hipSuccess) return e;
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(kfn), 64 * W, lds) !=
+                hipSuccess || per_cu < 1)
+            per_cu = 1;
+        const int64_t cap = (int64_t)per_cu * device_cu_count();
+        if (cap > 0 && cap < (int64_t)grid) grid = (unsigned)cap;
+        hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * W), lds, st, fa);
+        return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_any(int P, int R, int H, int W, const FArgs &fa, unsigned grid, hipStream_t st)
@@ -1135,5 +1184,6 @@ hipError_t unet_fused_step(const UnetFusedPlan &pl, const UnetFusedStep &s, hipS
     fa.prof = s.prof;
     const int64_t grid = (s.batch + pl.R / 2 - 1) / (pl.R / 2);
     if (grid <= 0 || grid > 0x7fffffff) return hipErrorInvalidValue;
+    fa.nblk = grid;
     return launch_any(pl.P, pl.R, pl.H, pl.W, fa, (unsigned)grid, st);
 }

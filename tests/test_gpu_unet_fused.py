@@ -36,6 +36,35 @@ def _eps_err(got, ref):
     return float((got.cpu() - ref).abs().max()) / max(float(ref.abs().max()), 1.0)
 
 
+def test_fused_h128_f16_panda_shape(fused):
+    """H = 128 (the Panda net's horizon: d = 7, C = 20) has a fused program with fp16 operands only (the three
+    split-bf16 planes of its activations do not fit one CU's LDS): against the oracle and the layered path, and the
+    f32x3 planner at this horizon refuses the forced fused form."""
+    d, H, C, B = 7, 128, 20, 3
+    net = make_unet(d, C, seed=128)
+    plan = _planner(net, d, H, C, N=25, dtype="f16")
+    assert plan.unet_form()["fused"]
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(B, H, d, generator=g)
+    ctx = torch.rand(1, C, generator=g) * 2 - 1
+    for t in (0, 13, 24):
+        ec, eu = plan.eps(x, t, ctx)
+        tt = torch.full((B,), t, dtype=torch.long)
+        with torch.no_grad():
+            rc = net(x, tt, ctx.expand(B, C), torch.zeros(B, 1))
+            ru = net(x, tt, ctx.expand(B, C), torch.ones(B, 1))
+        e1, e2 = _eps_err(ec, rc), _eps_err(eu, ru)
+        assert max(e1, e2) <= EPS_TOL["f16"], f"f16 H=128 t={t}: {e1:.2e} {e2:.2e}"
+        force_unet_path("layered")
+        lc, lu = plan.eps(x, t, ctx)
+        force_unet_path("fused")
+        assert _eps_err(ec, lc.cpu()) <= EPS_TOL["f16"] and _eps_err(eu, lu.cpu()) <= EPS_TOL["f16"]
+    full = plan.sample_trajectories(ctx, 5, H, seed=3, n_wo_noise=5)
+    assert torch.equal(full[2:4], plan.sample_trajectories(ctx, 2, H, seed=3, n_wo_noise=5, global_offset=2))
+    with pytest.raises(Exception):
+        _planner(net, d, H, C, N=25, dtype="f32x3").eps(x, 3, ctx)
+
+
 @pytest.mark.parametrize("dtype", ["f32x3", "f16"])
 @pytest.mark.parametrize("d,H,C,B", [(1, 32, 5, 24), (1, 32, 2, 37), (1, 64, 5, 6), (4, 64, 12, 5), (4, 64, 12, 131),
                                      (2, 32, 4, 16), (7, 32, 20, 9)])

@@ -67,6 +67,21 @@ def test_every_mfma_source_two_wait_states_after_a_valu_write(tmp_path):
     assert not bad, f"{len(bad)} MFMA sources written by a VALU op under 2 wait states: {bad[:3]}"
 
 
+def test_asm_mfma_results_wait_before_valu_reads(tmp_path):
+    """The other direction for the inline-asm MFMAs (AGPR operands): a VALU op may read an MFMA result only 8
+    wait states after it - what hipcc inserts after the builtin v_mfma_f32_16x16x32_bf16 (checked here too),
+    and what the asm statements of csrc/mlp_rw.hip write themselves."""
+    import mfma_hazard as mh
+    reads = mh.result_reads(_disassemble(tmp_path))
+    bf16 = [r for r in reads if r[1].startswith("v_mfma_f32_16x16x32_bf16")]
+    builtin = [r for r in bf16 if ", a[" not in r[1]]
+    asm = [r for r in bf16 if ", a[" in r[1]]
+    assert builtin and asm, "expected both builtin and AGPR-operand bf16 MFMAs"
+    assert min(r[3] for r in builtin) >= 8, "hipcc's own wait after the bf16 MFMA changed: revisit mlp_rw.hip"
+    close = [r for r in asm if r[3] < 8]
+    assert not close, f"{len(close)} VALU reads of an asm MFMA result under 8 wait states: {close[:3]}"
+
+
 def test_mfma_scan_finds_a_close_valu_write():
     import mfma_hazard as mh
     asm = ["_Z1kv:", "  v_mov_b32_e32 v31, v33", "  v_mfma_f32_16x16x32_bf16 v[28:31], a[20:23], v[0:3], v[28:31]",

@@ -79,6 +79,45 @@ def scan(lines, need=2):
     return bad
 
 
+def result_reads(lines, kernel_filter=None):
+    """[(kernel, mfma inst, first VALU reader of its result, wait states)] for every v_mfma_*: the walk forward
+    stops at the first VALU op that reads the destination (or overwrites it), a label or a branch."""
+    insts = instructions(lines)
+    out = []
+    for i, (k, t) in enumerate(insts):
+        if not t or not t.startswith("v_mfma") or (kernel_filter and kernel_filter not in (k or "")):
+            continue
+        ops = [x.strip() for x in t.split(None, 1)[1].split(",")]
+        dst, ws = regs(ops[0]), 0
+        for j in range(i + 1, min(len(insts), i + 64)):
+            _, u = insts[j]
+            if u is None or u.startswith("s_cbranch") or u.startswith("s_branch") or u.startswith("s_setpc"):
+                break
+            n = NOP.match(u)
+            if n:
+                ws += int(n.group(1)) + 1
+                continue
+            up = u.split(None, 1)
+            if len(up) > 1 and up[0].startswith("v_"):
+                uops = up[1].split(",")
+                if up[0].startswith("v_mfma"):
+                    if regs(",".join(uops[1:3])) & dst:  # read as srcA / srcB: not a forwarding case, report
+                        out.append((k, t, u, ws))
+                        break
+                    if regs(uops[0]) & dst and not regs(",".join(uops[3:4])) & dst:
+                        break  # overwritten
+                    if regs(",".join(uops[3:4])) & dst:
+                        break  # srcC of the next MFMA (forwarding): the chain continues there
+                else:
+                    if regs(",".join(uops[1:])) & dst:
+                        out.append((k, t, u, ws))
+                        break
+                    if regs(uops[0]) & dst:
+                        break
+            ws += 1
+    return out
+
+
 def main(argv):
     bad = scan(open(argv[1]).read().splitlines())
     for k, t, u, ws in bad[:20]:
