@@ -84,6 +84,10 @@ MPCD_DEV f32x4 mfma_agpr1(const u32x4 &w, const u32x4 &x, f32x4 acc)
 #ifndef MPCD_RW_ILV
 #define MPCD_RW_ILV 1
 #endif
+// MPCD_RW_EPI_STEPS = 1: the epilogue spread as 1-2 VALU ops per MFMA slot (hidden_ilv); 0: five units
+#ifndef MPCD_RW_EPI_STEPS
+#define MPCD_RW_EPI_STEPS 1
+#endif
 
 template <int D0, int SMODE, bool CTX, int R>
 struct MlpRw {
@@ -330,6 +334,68 @@ struct MlpRw {
         ldx(xb[0], 0);
         if (NI > 1) ldx(xb[1], 1);
         f32x4 acc = init_of(0), nxt = acc, ev = acc;
+#if MPCD_RW_EPI_STEPS
+        // The previous pass's epilogue as NSTEP micro-steps of one or two VALU instructions, one after each MFMA:
+        // a bf16 MFMA leaves the SIMD's vector issue free for 8 of its 16 cycles, i.e. about two VALU ops. Stage
+        // by stage over the four values (the dependent ops of one value 4 slots apart), the exact operations of
+        // common.h mish() and split3(); every intermediate through an empty register fence (no SLP packing).
+        float et[4];
+        u32x2 ep0, ep1, ep2;
+        f32x4 er = ev;
+        constexpr int NSTEP = (EPI != EPI_NONE ? 16 : 0) + 8;
+        auto fence = [](float &x) { asm volatile("" : "+v"(x)); };
+        auto epi_step = [&](int k, int p) {
+            if (EPI != EPI_NONE && k < 16) {
+                const int e = k & 3;
+                switch (k >> 2) {
+                case 0: et[e] = __builtin_amdgcn_exp2f(ev[e] * 1.44269504088896341f); fence(et[e]); break;
+                case 1: et[e] = __builtin_fmaf(et[e], et[e] + 2.0f, 2.0f); fence(et[e]); break;
+                case 2: et[e] = __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(et[e]), 1.0f); fence(et[e]); break;
+                default: { float y = ev[e] * et[e]; fence(y); ev[e] = y; } break;
+                }
+                return;
+            }
+            const int s = EPI != EPI_NONE ? k - 16 : k;
+            const int n = nt_of<l>(wave, jp(p)) * 16 + 4 * q;
+            char *o = lds + L::out_off(l) + (ct_of<l>(wave, cp(p)) * 16 + col) * L::out_rs(l) + n * 2;
+            switch (s) {  // split3 (mlp_x3.h), in pieces
+            case 0: ep0 = u32x2{pk_bf16(ev.x, ev.y), pk_bf16(ev.z, ev.w)}; break;
+            case 1: er.x = ev.x - bf_lo(ep0.x); er.y = ev.y - bf_hi(ep0.x); break;
+            case 2: er.z = ev.z - bf_lo(ep0.y); er.w = ev.w - bf_hi(ep0.y); *reinterpret_cast<u32x2 *>(o) = ep0; break;
+            case 3: ep1 = u32x2{pk_bf16(er.x, er.y), pk_bf16(er.z, er.w)}; break;
+            case 4: er.x = er.x - bf_lo(ep1.x); er.y = er.y - bf_hi(ep1.x); break;
+            case 5: er.z = er.z - bf_lo(ep1.y); er.w = er.w - bf_hi(ep1.y); break;
+            case 6: *reinterpret_cast<u32x2 *>(o + L::out_pl(l)) = ep1; ep2 = u32x2{pk_bf16(er.x, er.y), pk_bf16(er.z, er.w)}; break;
+            default: *reinterpret_cast<u32x2 *>(o + 2 * L::out_pl(l)) = ep2; break;
+            }
+        };
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            if (p + 1 < NP) nxt = init_of(p + 1);
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc) {
+                const int i = p * KC + kc;
+                if (i + 2 < NI) ldx(xb[(i + 2) % 3], i + 2);
+#pragma unroll
+                for (int m = 0; m < 6; ++m) {
+                    acc = mm1(jp(p), kc, m, xb[i % 3], acc);
+                    const int u = kc * 6 + m;
+                    if (p > 0 && u < NSTEP) epi_step(u, p - 1);
+                    if (i * 6 + m < NS) side(i * 6 + m);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            if (p > 0)
+#pragma unroll
+                for (int u = KC * 6; u < NSTEP; ++u) epi_step(u, p - 1);  // passes shorter than the epilogue
+            ev = acc;
+            acc = nxt;
+        }
+#pragma unroll
+        for (int u = 0; u < NSTEP; ++u) epi_step(u, NP - 1);
+#pragma unroll
+        for (int k = NI * 6; k < NS; ++k) side(k);
+#else
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
             if (p + 1 < NP) nxt = init_of(p + 1);
@@ -353,6 +419,7 @@ struct MlpRw {
         for (int u = 0; u < 5; ++u) epi_unit(u, ev, NP - 1);
 #pragma unroll
         for (int k = FREE<l>; k < NS; ++k) side(k);
+#endif
     }
 
     template <int l, int NS = 0, class SIDE>

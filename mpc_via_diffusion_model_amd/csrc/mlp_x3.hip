@@ -605,8 +605,10 @@ int mlp_x3_layout(int64_t batch, int nb)
              : !strcmp(e, "rw32") ? (int)LAYOUT_RW32 : !strcmp(e, "rw16") ? (int)LAYOUT_RW16 : -1;
     }();
     if (forced >= 0) return forced;
+    // below one 32-row workgroup per CU: 16-row workgroups of the resident-weight kernel (the 512-candidate
+    // strong-scaling shard: 0.89 vs 1.04 ms per control step for 16x8, profiles/r4_mlp_layouts.txt)
     const int n_cu = device_cu_count();
-    return (batch * nb + 31) / 32 < n_cu ? LAYOUT_16x8 : LAYOUT_32x8;
+    return (batch * nb + 31) / 32 < n_cu ? LAYOUT_RW16 : LAYOUT_32x8;
 }
 
 template <int D0, int SMODE, bool CTX>

@@ -40,7 +40,7 @@ def assert_traj_close(got, ref, rel=REL_TRAJ, abs_elem=ABS_ELEM, what="", spread
     if spread is not None:
         abs_elem = max(abs_elem, SPREAD_X * spread)
         log = os.environ.get("MPCD_SPREAD_LOG")
-        if log:
+        if log and spread > 0:
             with open(log, "a") as f:
                 f.write(f"{what}\t{el.max():.4e}\t{spread:.4e}\t{el.max() / max(spread, 1e-30):.3f}\t{tr.max():.4e}\n")
     assert tr.max() <= rel, f"{what}: worst trajectory rel err {tr.max():.3e} (> {rel})"
@@ -48,10 +48,12 @@ def assert_traj_close(got, ref, rel=REL_TRAJ, abs_elem=ABS_ELEM, what="", spread
     return tr.max(), el.max()
 
 
-# elementwise bar of an ill-conditioned chain (unclamped DDIM): this multiple of the oracle's own spread. Another
-# fp32-accurate implementation (split-bf16 GEMMs, its own reduction orders in the GroupNorm statistics) lands a
-# small multiple of that one-perturbation sample away; the trajectory bar (1e-4 relative) is not relaxed.
-SPREAD_X = 8
+# elementwise bar of an ill-conditioned chain (unclamped DDIM, the trained 30-step Panda / LMPC chains): this multiple
+# of the oracle's own spread. Another fp32-accurate implementation (split-bf16 GEMMs, its own reduction orders)
+# lands a small multiple of that one-perturbation sample away: measured at most 2.89x over every such test of the GPU
+# suite (profiles/r4_spread_ratios.tsv: MLP DDIM 2.89, MLP CFG-DDIM 2.36, fused U-Net CFG-DDIM 2.11, Panda 2.02,
+# LMPC 1.81), so the bar is that maximum rounded up; the trajectory bar (1e-4 relative) is not relaxed.
+SPREAD_X = 3
 
 
 def oracle_sensitivity(run):
