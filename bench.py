@@ -52,7 +52,7 @@ WORKLOADS = {
 PEAK_FP32 = 157.3e12      # MI355X dense fp32 MFMA / vector peak, FLOP/s (MI355X_MICROARCH.md)
 PEAK_BF16 = 2516.6e12     # MI355X dense bf16 / fp16 MFMA peak: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz
 PMC_FILES = {("cfg2", "f32"): os.path.join(ROOT, "profiles", "r1_pmc_mlp_sampler.json"),
-             ("cfg2", "f32x3"): os.path.join(ROOT, "profiles", "r3_pmc_mlp_x3.json"),
+             ("cfg2", "f32x3"): os.path.join(ROOT, "profiles", "r4_pmc_mlp_rw.json"),
              # U-Net: HBM bytes of one noise-net forward (the fused launch of one denoise step, PMC FETCH_SIZE x2 +
              # WRITE_SIZE, tools/unet_roofline.py) at B
              ("cfg3", "f32x3"): os.path.join(ROOT, "profiles", "r3_unet_roofline_cfg3.json"),

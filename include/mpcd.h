@@ -336,7 +336,7 @@ int mpcd_last_step_flags(mpcd_ctx *ctx, int32_t *flags);
  *              unless block_pick says otherwise;
  *   block_pick -1 = measured; -2 = never fuse; i >= 0 = fused candidate (i mod count) for every block. */
 int mpcd_unet_force_tiling(int32_t conv_pick, int32_t block_pick);
-/* MLP split-bf16 sampler workgroup layout (rows x waves), process-wide: -1 = by batch size (default: 32x8, or
+/* MLP split-bf16 sampler workgroup layout (rows x waves), process-wide: -1 = by batch size (default: rw32, or
  * rw16 when 32-row workgroups would leave CUs idle); 0 = 32x8; 1 = 16x8; 2 = 16x4 (two 4-wave workgroups per
  * CU where their LDS fits, else 16x8); 3 / 4 = rw32 / rw16 (csrc/mlp_rw.hip: 32 / 16 rows on 4 waves, the
  * 128-wide layers' weights resident in registers for the whole launch). All layouts compute the same sums in

@@ -605,10 +605,11 @@ int mlp_x3_layout(int64_t batch, int nb)
              : !strcmp(e, "rw32") ? (int)LAYOUT_RW32 : !strcmp(e, "rw16") ? (int)LAYOUT_RW16 : -1;
     }();
     if (forced >= 0) return forced;
-    // below one 32-row workgroup per CU: 16-row workgroups of the resident-weight kernel (the 512-candidate
-    // strong-scaling shard: 0.89 vs 1.04 ms per control step for 16x8, profiles/r4_mlp_layouts.txt)
+    // the resident-weight kernel (mlp_rw.hip) at every batch: 32-row workgroups (cfg2: 1.187 vs 1.252 ms kernel for
+    // the streaming 32x8), 16-row ones below one 32-row workgroup per CU (the 512-candidate strong-scaling shard:
+    // 0.87 vs 1.04 ms per control step for 16x8; cfg1 0.41 vs 0.49 ms kernel) - profiles/r4_mlp_layouts.txt
     const int n_cu = device_cu_count();
-    return (batch * nb + 31) / 32 < n_cu ? LAYOUT_RW16 : LAYOUT_32x8;
+    return (batch * nb + 31) / 32 < n_cu ? LAYOUT_RW16 : LAYOUT_RW32;
 }
 
 template <int D0, int SMODE, bool CTX>

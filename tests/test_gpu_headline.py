@@ -3,8 +3,8 @@
 bench.py's step is `plan.mpc_step(x0, double_int2d, B, w=0.01, seed=...)` with in-kernel Philox noise, the
 default (auto) MLP workgroup layout, the native one-call step (mpcd_mpc_step: sampler, chain-wide clip flag,
 fp64 rollout/cost fused with the argmin, winner row). Here that same call runs at BASELINE cfg 2 (B=4096,
-H=32, N=100: the 32-row x 8-wave `mlp_x3_kernel<64, DDPM_CFG, ctx, 32, 8>`) and cfg 1 (B=64, H=16, N=50:
-the resident-weight 16-row layout, mlp_rw_kernel<32, DDPM_CFG, ctx, 16>); every candidate's Philox draws are replayed (mpcd_philox_noise) through the oracle
+H=32, N=100: the resident-weight 32-row `mlp_rw_kernel<64, DDPM_CFG, ctx, 32>`) and cfg 1 (B=64, H=16, N=50:
+its 16-row form, mlp_rw_kernel<32, DDPM_CFG, ctx, 16>); every candidate's Philox draws are replayed (mpcd_philox_noise) through the oracle
 sampler (diffusion_model_base.py:181-209, sample_functions.py:17-44), the oracle LimitsNormalizer's
 chain-wide clip rule (normalization.py:156-167) and the C cost oracle, then argmin
 (scripts/inference/inference_(mpd).py:335-338). Bars: samples per trajectory 1e-4 and

@@ -71,15 +71,16 @@ run_job() {
       local c=${arg:-cfg5}
       timeout -k 10 600 python -u tools/unet_perf.py ${UARGS[$c]} $UNET_ARGS > "gpurun_out/unet_$c.log" 2>&1 ;;
     upmc)
+      # $UPMC_TAG: suffix of the output names (A/B of an environment switch, e.g. MPCD_FUSED_PERSIST=1)
       local c=${arg:-cfg5} i=0 ctr
-      local a="${UARGS[$c]} --steps 1 --reps 1 $UNET_ARGS"
-      export MPCD_UNET_TUNE_CACHE=gpurun_out/uroof/${c}_tune.txt
+      local a="${UARGS[$c]} --steps 1 --reps 1 $UNET_ARGS" n=${arg:-cfg5}$UPMC_TAG
+      export MPCD_UNET_TUNE_CACHE=gpurun_out/uroof/${n}_tune.txt
       rm -f "$MPCD_UNET_TUNE_CACHE"
-      timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d "gpurun_out/uroof/${c}_trace" -o run -f csv -- \
-        python3 tools/unet_perf.py $a > "gpurun_out/uroof/${c}_trace.log" 2>&1 || return $?
+      timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d "gpurun_out/uroof/${n}_trace" -o run -f csv -- \
+        python3 tools/unet_perf.py $a > "gpurun_out/uroof/${n}_trace.log" 2>&1 || return $?
       for ctr in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE"; do
-        timeout -s KILL 300 rocprofv3 --pmc $ctr -d "gpurun_out/uroof/${c}_p$i" -o run -f csv -- \
-          python3 tools/unet_perf.py $a > "gpurun_out/uroof/${c}_p$i.log" 2>&1 || return $?
+        timeout -s KILL 300 rocprofv3 --pmc $ctr -d "gpurun_out/uroof/${n}_p$i" -o run -f csv -- \
+          python3 tools/unet_perf.py $a > "gpurun_out/uroof/${n}_p$i.log" 2>&1 || return $?
         i=$((i + 1))
       done
       unset MPCD_UNET_TUNE_CACHE ;;

@@ -23,7 +23,7 @@ def main(fetch_dir, write_dir, label, out, only=None):
     warm_f = sum(f[1:]) / len(f[1:])
     warm_w = sum(w[1:]) / len(w[1:])
     res = {"kernel": kname, "label": label,
-           "command": "rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE --kernel-include-regex 'mlp_(x3|sample)_kernel' -- "
+           "command": "rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE -- "
                       "python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --dtype <dt> (one pass per counter)",
            "FETCH_SIZE_kb_per_launch": f, "WRITE_SIZE_kb_per_launch": w,
            "hbm_bytes_per_launch": int((2 * warm_f + warm_w) * 1024),
