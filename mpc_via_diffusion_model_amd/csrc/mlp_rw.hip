@@ -391,8 +391,14 @@ struct MlpRw {
             ev = acc;
             acc = nxt;
         }
+#ifndef MPCD_RW_EXP_NOLASTEPI
+#define MPCD_RW_EXP_NOLASTEPI 0
+#endif
+        // MPCD_RW_EXP_NOLASTEPI (timing experiment only, wrong results): drop the exposed last-pass epilogue of
+        // the multi-pass layers - the bound on what deferring it into the next layer could gain
+        if (!(MPCD_RW_EXP_NOLASTEPI && NP >= 2))
 #pragma unroll
-        for (int u = 0; u < NSTEP; ++u) epi_step(u, NP - 1);
+            for (int u = 0; u < NSTEP; ++u) epi_step(u, NP - 1);
 #pragma unroll
         for (int k = NI * 6; k < NS; ++k) side(k);
 #else
@@ -659,7 +665,11 @@ struct MlpRw {
             bk = bk == 13 ? 0 : bk + 1;
         };
 #else
+#if MPCD_RW_EXP_BAR2
+        auto bar = [] { lds_barrier(); lds_barrier(); };  // timing experiment: the cost of one more barrier per layer
+#else
         auto bar = [] { lds_barrier(); };
+#endif
 #endif
 
         for (int s = 0; s < p.n_steps; ++s) {
