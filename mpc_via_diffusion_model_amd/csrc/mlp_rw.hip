@@ -89,6 +89,12 @@ MPCD_DEV f32x4 mfma_agpr1(const u32x4 &w, const u32x4 &x, f32x4 acc)
 #define MPCD_RW_EPI_STEPS 1
 #endif
 
+// timing experiments (wrong results): MPCD_RW_EXP_NOLASTEPI drops the last-pass epilogue of the multi-pass
+// layers (hidden_ilv); MPCD_RW_EXP_BAR2 doubles every layer barrier (profiles/r4_mlp_defer_ab.txt)
+#ifndef MPCD_RW_EXP_NOLASTEPI
+#define MPCD_RW_EXP_NOLASTEPI 0
+#endif
+
 template <int D0, int SMODE, bool CTX, int R>
 struct MlpRw {
     static constexpr int NB = (SMODE == MODE_DDIM || SMODE == MODE_EPS1) ? 1 : 2;
@@ -391,9 +397,6 @@ struct MlpRw {
             ev = acc;
             acc = nxt;
         }
-#ifndef MPCD_RW_EXP_NOLASTEPI
-#define MPCD_RW_EXP_NOLASTEPI 0
-#endif
         // MPCD_RW_EXP_NOLASTEPI (timing experiment only, wrong results): drop the exposed last-pass epilogue of
         // the multi-pass layers - the bound on what deferring it into the next layer could gain
         if (!(MPCD_RW_EXP_NOLASTEPI && NP >= 2))
@@ -618,6 +621,11 @@ struct MlpRw {
         float *bic = reinterpret_cast<float *>(lds + L::BIC);
         float *cps = reinterpret_cast<float *>(lds + L::CPS);
 
+#if MPCD_RW_EXP_NOLASTEPI
+        // the timing experiment leaves output tiles unwritten: start from a zeroed LDS so they read finite values
+        for (int i = threadIdx.x; i < L::total / 16; i += RW_T) reinterpret_cast<u32x4 *>(lds)[i] = u32x4{0u, 0u, 0u, 0u};
+        lds_barrier();
+#endif
         Res res;
         load_res(res, wp, wave, lane);
         for (int l = 0; l < NLAYER; ++l)
