@@ -205,6 +205,16 @@ class DiffusionMPC:
         return out
 
     # ------------------------------------------------------------------ sampling (A2-A11)
+    def _system_desc(self, system):
+        """system.desc() (a ctypes struct), rebuilt only when the system's fields change: a control loop calls
+        mpc_step with the same system every step."""
+        key = (system.system, system.cost_kind, system.n_x, system.n_u, tuple(system.params), tuple(system.Q),
+               tuple(system.R), tuple(system.P), tuple(system.x_ref))
+        c = getattr(self, "_desc_cache", None)
+        if c is None or c[0] != key:
+            c = self._desc_cache = (key, system.desc())
+        return c[1]
+
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
@@ -489,8 +499,8 @@ class DiffusionMPC:
         if d != system.n_u:
             raise ValueError(f"system {system.name} has {system.n_u} inputs, samples have {d}")
         sampler = self._sampler_id(sample_fn)
-        steps = self.n_denoise_steps(sample_fn, n_wo_noise, ddim_steps)
         if noise is not None:
+            steps = self.n_denoise_steps(sample_fn, n_wo_noise, ddim_steps)
             noise = noise.to(self.device, torch.float32).contiguous()
             if tuple(noise.shape) != (steps + 1, B, H, d):
                 raise ValueError(f"noise must be [{steps + 1}, {B}, {H}, {d}], got {tuple(noise.shape)}")
@@ -498,7 +508,7 @@ class DiffusionMPC:
         cost = torch.empty(B, dtype=torch.float64, device=self.device)
         costs = torch.empty(size * B, dtype=torch.float64, device=self.device) if size > 1 else cost
         x0 = np.ascontiguousarray(x0, dtype=np.float64)
-        desc = system.desc()
+        desc = self._system_desc(system)
         a = N.StepArgs()
         a.sys = ctypes.pointer(desc)
         a.x0 = x0.ctypes.data
