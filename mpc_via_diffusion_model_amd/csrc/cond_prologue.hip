@@ -75,7 +75,29 @@ __global__ __launch_bounds__(256) void ctx_prologue_kernel(const float *ctx, int
     cproj[i] = (float)acc;
 }
 
+// ctx_prologue_kernel for one shared row given by value
+__global__ __launch_bounds__(256) void ctx_prologue_row_kernel(const CtxRowArg row, int ctx_dim, const CondLayer *layers,
+                                                               int n_layers, int cond_dim, int cond_total, float *cproj)
+{
+    const int col = blockIdx.x * blockDim.x + threadIdx.x;
+    if (col >= cond_total) return;
+    int l = 0;
+    while (l + 1 < n_layers && layers[l + 1].off <= col) ++l;
+    const CondLayer L = layers[l];
+    const int n = col - L.off;
+    double acc = 0.0;
+    for (int k = 0; k < ctx_dim; ++k) acc += (double)L.W[(size_t)n * cond_dim + TDIM + k] * (double)mish_precise(row.v[k]);
+    cproj[col] = (float)acc;
+}
+
 }  // namespace
+
+void launch_ctx_prologue_row(const CtxRowArg &row, int ctx_dim, const CondLayer *layers_dev, int n_layers,
+                             int cond_dim, int cond_total, float *cproj, hipStream_t stream)
+{
+    hipLaunchKernelGGL(ctx_prologue_row_kernel, dim3((unsigned)((cond_total + 255) / 256)), dim3(256), 0, stream, row,
+                       ctx_dim, layers_dev, n_layers, cond_dim, cond_total, cproj);
+}
 
 void launch_time_prologue(const StepPlan *plan, int n_steps, const float *time_w1, const float *time_b1,
                           const float *time_w2, const float *time_b2, const CondLayer *layers_dev, int n_layers,

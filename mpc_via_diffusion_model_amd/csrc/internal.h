@@ -25,6 +25,13 @@ void launch_time_prologue(const StepPlan *plan, int n_steps, const float *time_w
 // Context prologue: cproj[b][off_j + n] = cond_mlp_j.W[n, T:] . Mish(ctx_b)   (no bias)
 void launch_ctx_prologue(const float *ctx, int64_t n_rows, int ctx_dim, const CondLayer *layers_dev, int n_layers,
                          int cond_dim, int cond_total, float *cproj, hipStream_t stream);
+// one shared context row passed by value (mpcd_mpc_step: no host-to-device copy before the sampler)
+constexpr int kCtxRowMax = 64;
+struct CtxRowArg {
+    float v[kCtxRowMax];
+};
+void launch_ctx_prologue_row(const CtxRowArg &row, int ctx_dim, const CondLayer *layers_dev, int n_layers,
+                             int cond_dim, int cond_total, float *cproj, hipStream_t stream);
 
 // The samplers' Philox noise stream for candidates [goff, goff + n): out [n_slices][n][flat] (mpcd_philox_noise)
 hipError_t launch_philox_noise(uint64_t seed, int64_t goff, int64_t n, int n_slices, int flat, float *out,
@@ -84,6 +91,7 @@ hipError_t launch_mlp_x3(int d0, int nb, const MlpSampleArgs &a, hipStream_t str
 hipError_t launch_mlp_rw(int d0, int rows, const MlpSampleArgs &a, hipStream_t stream);
 
 // Fused selection for launch_rollout_cost (single rank): see rollout.hip SelectK
+constexpr int64_t kFuseClipMax = 16384;  // clip inputs up to this many floats are tested inside the selecting launch
 struct RolloutSelect {
     mpcd_best *best;
     float *row_out;
@@ -93,5 +101,9 @@ struct RolloutSelect {
     int64_t n_part;       // capacity of part_* (>= ceil(batch / 64))
     int64_t offset;
     int32_t *code_out;    // optional: the clip code flags[0], written with the winner (mpcd_mpc_step's result block)
+    // optional: the clip code is computed in this launch, by every workgroup, over clip_src[0, clip_n) (the
+    // clip_flag_kernel test; a small batch's per-candidate chain maxima) instead of read from flag_dev
+    const float *clip_src;
+    int64_t clip_n;
 };
 constexpr int kRolloutBlock = 64;  // candidates per rollout workgroup

@@ -586,7 +586,16 @@ int mpcd_sample_steps(mpcd_ctx *c, const mpcd_sample_args *a, int32_t *n)
     return MPCD_OK;
 }
 
+// ctx_row: mpcd_mpc_step's one shared context row by value (the ctx prologue reads it from its kernel
+// arguments: no host-to-device copy); nullptr: a->context on the device (the C-ABI mpcd_sample)
+static int sample_impl(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr, const CtxRowArg *ctx_row);
+
 int mpcd_sample(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr)
+{
+    return sample_impl(c, a, stream_ptr, nullptr);
+}
+
+static int sample_impl(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr, const CtxRowArg *ctx_row)
 {
     if (!c || !a) return fail(MPCD_EINVAL, "null argument");
     if (!c->net_loaded) return fail(MPCD_ESTATE, "no net loaded");
@@ -596,7 +605,7 @@ int mpcd_sample(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr)
     const bool cfg = a->sampler == MPCD_DDPM_CFG || a->sampler == MPCD_DDIM_CFG;
     if (a->sampler < 0 || a->sampler > MPCD_DDIM) return fail(MPCD_EINVAL, "bad sampler %d", a->sampler);
     if (cfg != (d.cfg_masked != 0)) return fail(MPCD_EINVAL, "CFG samplers need a cfg_masked net and vice versa");
-    if (d.context_dim > 0 && !a->context) return fail(MPCD_EINVAL, "net has a context but none given");
+    if (d.context_dim > 0 && !a->context && !ctx_row) return fail(MPCD_EINVAL, "net has a context but none given");
     hipStream_t st = static_cast<hipStream_t>(stream_ptr);
     DEVICE_GUARD(c->device);
 
@@ -626,13 +635,18 @@ int mpcd_sample(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr)
     const float *cproj = nullptr;
     int64_t cstride = 0;
     if (d.context_dim > 0) {
-        const int64_t rows = a->context_shared ? 1 : a->batch;
+        const bool shared = ctx_row || a->context_shared;
+        const int64_t rows = shared ? 1 : a->batch;
         if ((rc = c->cproj.ensure(sizeof(float) * (size_t)rows * c->cond_total))) return rc;
-        launch_ctx_prologue(a->context, rows, d.context_dim, cl, c->n_cond, c->cond_dim, c->cond_total,
-                            c->cproj.as<float>(), st);
+        if (ctx_row)
+            launch_ctx_prologue_row(*ctx_row, d.context_dim, cl, c->n_cond, c->cond_dim, c->cond_total,
+                                    c->cproj.as<float>(), st);
+        else
+            launch_ctx_prologue(a->context, rows, d.context_dim, cl, c->n_cond, c->cond_dim, c->cond_total,
+                                c->cproj.as<float>(), st);
         HIP_TRY(hipGetLastError());
         cproj = c->cproj.as<float>();
-        cstride = a->context_shared ? 0 : c->cond_total;
+        cstride = shared ? 0 : c->cond_total;
     }
     const float wp1 = (float)(1.0 + a->w), wf = (float)a->w;
     HIP_TRY(hipEventRecord(c->ev0, st));
@@ -1096,14 +1110,17 @@ int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, fl
 
     // normalize_condition (A12), fp64 then the net's .float()
     mpcd_sample_args sa = a->sample;
+    CtxRowArg ctx_row{};
+    const bool by_value = d.context_dim > 0 && d.context_dim <= kCtxRowMax;
     if (d.context_dim > 0) {
-        float *ch = static_cast<float *>(c->step_host);
+        float *ch = by_value ? ctx_row.v : static_cast<float *>(c->step_host);
         for (int i = 0; i < d.context_dim; ++i) {
             const double den = (double)(a->ctx_max[i] - a->ctx_min[i]);
             ch[i] = (float)(2.0 * ((a->x0[i] - (double)a->ctx_min[i]) / den) - 1.0);
         }
-        HIP_TRY(hipMemcpyAsync(c->step_ctx.p, ch, sizeof(float) * d.context_dim, hipMemcpyHostToDevice, st));
-        sa.context = c->step_ctx.as<float>();
+        if (!by_value)
+            HIP_TRY(hipMemcpyAsync(c->step_ctx.p, ch, sizeof(float) * d.context_dim, hipMemcpyHostToDevice, st));
+        sa.context = by_value ? nullptr : c->step_ctx.as<float>();
         sa.context_shared = 1;
     } else {
         sa.context = nullptr;
@@ -1113,13 +1130,18 @@ int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, fl
         if ((rc = c->step_amax.ensure(sizeof(float) * (size_t)B))) return rc;
         sa.chain_absmax = c->step_amax.as<float>();
     }
-    if ((rc = mpcd_sample(c, &sa, stream))) return rc;
+    if ((rc = sample_impl(c, &sa, stream, by_value ? &ctx_row : nullptr))) return rc;
 
     // LimitsNormalizer's global clip flag over the chain (the reference's unnormalize_states of run_CFG's
     // whole chain), over the final samples, or proven 0; max-reduced over ranks (see mpcd_clip_flag)
     int *flags = c->flag.as<int>();
     const int *flag = flags + 1;  // flag[1] is never written: a constant 0
-    if (a->clip_rule != MPCD_CLIP_NONE) {
+    // single rank, a small clip input: the selecting rollout launch computes the clip code itself (each
+    // workgroup over the whole input, <= kFuseClipMax floats) - one launch fewer per control step
+    const float *clip_src = a->clip_rule == MPCD_CLIP_CHAIN ? sa.chain_absmax : sa.x_out;
+    const int64_t clip_n = a->clip_rule == MPCD_CLIP_CHAIN ? B : B * row;
+    const bool fuse_clip = !c->comm && a->clip_rule != MPCD_CLIP_NONE && clip_n <= kFuseClipMax;
+    if (a->clip_rule != MPCD_CLIP_NONE && !fuse_clip) {
         if (a->clip_rule == MPCD_CLIP_CHAIN)
             HIP_TRY(launch_clip_flag(sa.chain_absmax, B, flags, c->sync_ws(), st));
         else
@@ -1133,7 +1155,8 @@ int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, fl
     int64_t *part_idx = reinterpret_cast<int64_t *>(part_cost + n_part);
     int32_t *code_dev = reinterpret_cast<int32_t *>(u_dev + row);
     if (!c->comm) {  // rollout + cost + argmin + the winner's unnormalised row + the clip code in one launch
-        RolloutSelect sel{best_dev, u_dev, part_cost, part_idx, c->sync_ws() + 8, n_part, sa.global_offset, code_dev};
+        RolloutSelect sel{best_dev, u_dev,    part_cost, part_idx, c->sync_ws() + 8, n_part, sa.global_offset, code_dev,
+                          fuse_clip ? clip_src : nullptr, fuse_clip ? clip_n : 0};
         HIP_TRY(launch_rollout_cost(sys, a->x0, nullptr, B, sa.x_out, a->act_min, a->act_max, flag, B, H,
                                     a->cost_local, st, &sel));
     } else {

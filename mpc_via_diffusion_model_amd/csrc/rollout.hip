@@ -42,6 +42,8 @@ struct SelectK {
     unsigned *counter;
     int64_t offset;      // global index of candidate 0
     int32_t *code_out;   // optional: flags[0] copied next to the winner (saves the caller a device copy)
+    const float *clip_src;  // optional: the clip code computed here over clip_src[0, clip_n) (RolloutSelect)
+    int64_t clip_n;
 };
 
 // (v, i) beats (bv, bi): NaN = +inf, lower cost, then lower index; i < 0 = empty
@@ -237,9 +239,29 @@ __global__ __launch_bounds__(RT_THREADS) void rollout_cost_kernel(const SysK S, 
             su[c * stride + k] = src[i];
         }
     }
+    int code = 0;  // SEL with clip_src: the clip code, recomputed by every workgroup (clip_flag_kernel's test)
+    if constexpr (SEL) {
+        if (K.clip_src) {
+            const float hi = (float)(1.0 + 1e-4), lo = (float)(-1.0 - 1e-4);
+            unsigned any = 0;
+            const int64_t n4 = ((uintptr_t)K.clip_src & 15) ? 0 : K.clip_n >> 2;
+            for (int64_t i = threadIdx.x; i < n4; i += RT_THREADS) {
+                const f32x4 v = ldg4(K.clip_src + 4 * i);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) any |= clip_bits(v[e], hi, lo);
+            }
+            for (int64_t i = 4 * n4 + threadIdx.x; i < K.clip_n; i += RT_THREADS) any |= clip_bits(K.clip_src[i], hi, lo);
+            __shared__ unsigned blk;
+            if (threadIdx.x == 0) blk = 0;
+            __syncthreads();
+            if (any) atomicOr(&blk, any);
+            __syncthreads();
+            code = clip_code(blk);
+        }
+    }
     __syncthreads();
     const int64_t b = min(c0 + threadIdx.x, batch - 1);  // lanes past the batch recompute the last one
-    const bool clip = flags[b / group] == 1;
+    const bool clip = (SEL && K.clip_src) ? code == 1 : flags[b / group] == 1;
     float mn[nu], mx[nu];
 #pragma unroll
     for (int i = 0; i < nu; ++i) { mn[i] = S.umin[i]; mx[i] = S.umax[i]; }
@@ -304,10 +326,10 @@ __global__ __launch_bounds__(RT_THREADS) void rollout_cost_kernel(const SysK S, 
             K.best->cost = v;
             K.best->index = i < 0 ? -1 : K.offset + i;
             *K.counter = 0u;
-            if (K.code_out) *K.code_out = flags[0];
+            if (K.code_out) *K.code_out = K.clip_src ? code : flags[0];
         }
         if (i >= 0 && K.row_out) {
-            const bool clip0 = flags[0] == 1;
+            const bool clip0 = K.clip_src ? code == 1 : flags[0] == 1;
             for (int k = threadIdx.x; k < row; k += RT_THREADS)
                 K.row_out[k] = unnorm1(u_norm[(size_t)i * row + k], clip0, S.umin[k % nu], S.umax[k % nu]);
         }
@@ -509,7 +531,8 @@ hipError_t launch_rollout_cost(const mpcd_system_desc &d, const double *x0_host,
     SelectK K = {};
     if (sel) {
         if (group != batch || sel->n_part < (batch + RT_THREADS - 1) / RT_THREADS) return hipErrorInvalidValue;
-        K = SelectK{sel->best, sel->row_out, sel->part_cost, sel->part_idx, sel->counter, sel->offset, sel->code_out};
+        K = SelectK{sel->best,   sel->row_out, sel->part_cost, sel->part_idx, sel->counter,
+                    sel->offset, sel->code_out, sel->clip_src,  sel->clip_n};
     }
     const dim3 grid((unsigned)((batch + RT_THREADS - 1) / RT_THREADS));
 #define MPCD_ROLLOUT(SYS_)                                                                                          \
