@@ -495,10 +495,26 @@ struct MlpRw {
     static constexpr int NZT = TL<13>;
 
     // final Linear (32 -> D0) + the denoise update (reference op order, mlp_x3.hip final_and_update)
+#ifdef MPCD_PROF_LAYERS
+#define MPCD_FINAL_PROF , uint64_t(&tacc)[32]
+#define MPCD_FINAL_MARK(k, dep)                                                                                      \
+    do {                                                                                                             \
+        asm volatile("" ::"v"(dep) : "memory");                                                                     \
+        const uint64_t t_ = __builtin_readcyclecounter();                                                            \
+        tacc[k] += t_ - tmark;                                                                                       \
+        tmark = t_;                                                                                                  \
+    } while (0)
+#else
+#define MPCD_FINAL_PROF
+#define MPCD_FINAL_MARK(k, dep)
+#endif
     static MPCD_DEV void final_and_update(const FW &f, char *lds, const MlpSampleArgs &p, const StepPlan &sp, int s,
                                           int64_t cand0, const f32x4 (&nz)[NZT][NB], uint32_t (&am)[2], int wave,
-                                          int lane)
+                                          int lane MPCD_FINAL_PROF)
     {
+#ifdef MPCD_PROF_LAYERS
+        uint64_t tmark = __builtin_readcyclecounter();
+#endif
         constexpr int T = NZT, NT = D0 / 16;
         const int col = lane & 15, q = lane >> 4;
         const float *bias = reinterpret_cast<const float *>(lds + L::BI + A::boff(13) * 4);
@@ -516,6 +532,12 @@ struct MlpRw {
             for (int j = 0; j < T; ++j)
                 if (NT % 4 == 0 || wave + 4 * j < NT) acc[j][c] = mfma_x3(f.v[j][0], x, acc[j][c]);
         }
+        MPCD_FINAL_MARK(28, acc[0][1]);  // experiment build: the final layer's operand reads and MFMAs
+#ifdef MPCD_PROF_FINAL_MFMA_ONLY
+        // timing experiment (wrong results): the final layer's MFMAs only, no update
+        if (acc[0][0][0] == 12345.f && acc[0][1][1] == 54321.f) am[0] = 1u;
+        return;
+#endif
         if (R == 16 && NB == 2) {
             // column c holds candidate c & 7's context row (c < 8) or masked row (c >= 8): bring the masked
             // row's eps next to the context row's (DPP row_ror:8 swaps the two halves of each 16-lane row)
@@ -581,6 +603,7 @@ struct MlpRw {
                 }
             }
         }
+        MPCD_FINAL_MARK(29, am[0]);  // experiment build: the update, the stores
     }
 
     // noise of step s (slice s+1) for this lane's quads, fetched one step ahead of use
@@ -606,6 +629,83 @@ struct MlpRw {
             else
                 nz[j][0] = philox_normal4(p.seed, (uint64_t)(p.global_offset + gc), (uint32_t)(s + 1), (uint32_t)(n >> 2));
         }
+    }
+
+    // The next step's Philox draw (CFG-DDPM with in-kernel noise, one quad per lane) as NPH micro-steps, issued
+    // as side work in Linear 8's MFMA slots instead of in the open after Linear 10 (~880 cycles per step there):
+    // the exact operations of common.h philox4x32_10 / philox_normal4, one quarter-rate multiply per step,
+    // every intermediate through a register fence. Bit-identical to fetch_noise.
+    struct PhSt {
+        uint32_t c0, c1, c2, c3, k0, k1, h;
+        float u0, u1, u2, u3, ra, rb;
+        float z[4];
+    };
+    static constexpr int NPH = 40 + 12;
+    static constexpr bool STAGED_NOISE = SMODE == MODE_DDPM_CFG && NZT == 1;
+    static MPCD_DEV void ph_init(PhSt &st, const MlpSampleArgs &p, int slice, int64_t cand0, int wave, int lane)
+    {
+        const int col = lane & 15, q = lane >> 4;
+        const int n = min(wave, D0 / 16 - 1) * 16 + 4 * q;  // clamped tile: lanes past NT draw and discard
+        const uint64_t cand = (uint64_t)(p.global_offset + cand0 + col);
+        st.c0 = (uint32_t)(n >> 2);
+        st.c1 = (uint32_t)cand;
+        st.c2 = (uint32_t)(cand >> 32);
+        st.c3 = (uint32_t)slice;
+        st.k0 = (uint32_t)p.seed;
+        st.k1 = (uint32_t)(p.seed >> 32);
+    }
+    static MPCD_DEV void ph_step(PhSt &st, int k)
+    {
+        auto fu = [](uint32_t &x) { asm volatile("" : "+v"(x)); };
+        auto ff = [](float &x) { asm volatile("" : "+v"(x)); };
+        constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+        if (k < 40) {  // round k / 4 of philox4x32_10
+            switch (k & 3) {
+            case 0: st.h = __umulhi(M0, st.c0); fu(st.h); break;                  // hi0
+            case 1: st.c0 = M0 * st.c0; fu(st.c0); break;                         // lo0 (in c0 until the swap)
+            case 2: { const uint32_t hi1 = __umulhi(M1, st.c2); st.c3 = st.h ^ st.c3 ^ st.k1; st.h = hi1; fu(st.h); fu(st.c3); } break;
+            default: {
+                const uint32_t lo1 = M1 * st.c2;
+                // c' = (hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0); c3 holds hi0 ^ c3 ^ k1, c0 holds lo0
+                const uint32_t n0 = st.h ^ st.c1 ^ st.k0, n2 = st.c3, n3 = st.c0;
+                st.c0 = n0; st.c1 = lo1; st.c2 = n2; st.c3 = n3;
+                st.k0 += W0; st.k1 += W1;
+                fu(st.c0); fu(st.c1); fu(st.c2); fu(st.c3);
+            } break;
+            }
+            return;
+        }
+        const float S = 2.3283064365386963e-10f;  // 2^-32
+        switch (k - 40) {  // philox_normal4's Box-Muller
+        case 0: st.u0 = ((float)st.c0 + 1.0f) * S; st.u1 = (float)st.c1 * S; ff(st.u0); ff(st.u1); break;
+        case 1: st.u2 = ((float)st.c2 + 1.0f) * S; st.u3 = (float)st.c3 * S; ff(st.u2); ff(st.u3); break;
+        case 2: st.ra = -2.0f * __logf(st.u0); ff(st.ra); break;
+        case 3: st.rb = -2.0f * __logf(st.u2); ff(st.rb); break;
+        case 4: st.ra = __fsqrt_rn(st.ra); ff(st.ra); break;
+        case 5: st.rb = __fsqrt_rn(st.rb); ff(st.rb); break;
+        case 6: st.u1 = 6.2831853071795865f * st.u1; st.u3 = 6.2831853071795865f * st.u3; ff(st.u1); ff(st.u3); break;
+        case 7: st.z[0] = __cosf(st.u1); ff(st.z[0]); break;
+        case 8: st.z[1] = __sinf(st.u1); ff(st.z[1]); break;
+        case 9: st.z[2] = __cosf(st.u3); ff(st.z[2]); break;
+        case 10: st.z[3] = __sinf(st.u3); ff(st.z[3]); break;
+        default:
+            for (int e = 0; e < 4; ++e) {
+                st.z[e] = (e < 2 ? st.ra : st.rb) * st.z[e];
+                ff(st.z[e]);
+            }
+            break;
+        }
+    }
+    // fetch_noise's result from the staged draw: zeros where fetch_noise draws none
+    static MPCD_DEV void ph_take(f32x4 (&nz)[NZT][NB], const PhSt &st, const StepPlan &sp, int64_t cand0,
+                                 const MlpSampleArgs &p, int wave, int lane)
+    {
+        const int col = lane & 15;
+#pragma unroll
+        for (int g = 0; g < NB; ++g) nz[0][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const bool ok = (sp.flags & PLAN_NOISE) && (D0 / 16 % 4 == 0 || wave < D0 / 16) && cand0 + col < p.batch &&
+                        !(R == 16 && col >= 8);
+        if (ok) nz[0][0] = f32x4{st.z[0], st.z[1], st.z[2], st.z[3]};
     }
 
     static MPCD_DEV void run(const MlpSampleArgs &p)
@@ -727,7 +827,15 @@ struct MlpRw {
             load_ws<9>(w9, ws, wave, lane16);
             bar();
             WS<10> w10;
-            layer<8>(w8, none, lds, wave, lane);
+            const StepPlan cur = sp;
+            if (s + 1 < p.n_steps) sp = load_plan(p.plan, s + 1);
+            PhSt ph;
+            if constexpr (STAGED_NOISE) {
+                ph_init(ph, p, s + 2, cand0, wave, lane);  // step s + 1's noise is Philox slice s + 2 (fetch_noise)
+                layer<8, NPH>(w8, [&](int k) { ph_step(ph, k); }, lds, wave, lane);
+            } else {
+                layer<8>(w8, none, lds, wave, lane);
+            }
             load_ws<10>(w10, ws, wave, lane16);  // after L8: w8's 96 registers are free again
             bar();
             WS<11> w11;
@@ -743,15 +851,22 @@ struct MlpRw {
                 lds, wave, lane);
             bar();
             layer<10>(w10, none, lds, wave, lane);
-            const StepPlan cur = sp;
             f32x4 nzc[NZT][NB];
 #pragma unroll
             for (int j = 0; j < NZT; ++j)
 #pragma unroll
                 for (int g = 0; g < NB; ++g) nzc[j][g] = nz[j][g];
-            if (s + 1 < p.n_steps) {
-                sp = load_plan(p.plan, s + 1);
+            if (STAGED_NOISE && s + 1 < p.n_steps) {
+                ph_take(nz, ph, sp, cand0, p, wave, lane);
+            } else if (s + 1 < p.n_steps) {
+#ifdef MPCD_PROF_LAYERS
+                const uint64_t tn0 = __builtin_readcyclecounter();
+#endif
                 fetch_noise(nz, p, sp, s + 1, cand0, wave, lane);
+#ifdef MPCD_PROF_LAYERS
+                asm volatile("" ::: "memory");
+                tacc[31] += __builtin_readcyclecounter() - tn0;  // "tail" row, wait column: the noise draws
+#endif
             }
             load_ws<0>(w0, ws, wave, lane16);  // next step's layer 0 (unconditional: path-independent load count)
             bar();
@@ -759,7 +874,11 @@ struct MlpRw {
             bar();
             layer<12>(w12, none, lds, wave, lane);
             bar();
+#ifdef MPCD_PROF_LAYERS
+            final_and_update(w13, lds, p, cur, s, cand0, nzc, am, wave, lane, tacc);  // "-" row: MFMAs / update
+#else
             final_and_update(w13, lds, p, cur, s, cand0, nzc, am, wave, lane);
+#endif
         }
 #ifdef MPCD_PROF_LAYERS
         {
