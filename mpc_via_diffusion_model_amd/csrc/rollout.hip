@@ -245,7 +245,8 @@ __global__ __launch_bounds__(RT_THREADS) void rollout_cost_kernel(const SysK S, 
             const float hi = (float)(1.0 + 1e-4), lo = (float)(-1.0 - 1e-4);
             unsigned any = 0;
             const int64_t n4 = ((uintptr_t)K.clip_src & 15) ? 0 : K.clip_n >> 2;
-            for (int64_t i = threadIdx.x; i < n4; i += RT_THREADS) {
+#pragma unroll 8
+            for (int64_t i = threadIdx.x; i < n4; i += RT_THREADS) {  // unrolled: eight loads in flight per lane
                 const f32x4 v = ldg4(K.clip_src + 4 * i);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) any |= clip_bits(v[e], hi, lo);
