@@ -6,10 +6,14 @@ noise-net (build-defined CFG MLP), fp32-accurate GEMMs. One ste
 i.e. one mpcd_mpc_step call: context upload, Philox x_T + the denoising loop (2 net evaluations per
 step) + clip flag + fp64 rollout/cost + argmin + winner row (+ RCCL cost all-gather and winner
 exchange for N > 1) + one D2H copy of the applied trajectory. Weak scaling: every rank adds its
-candidates.
+4096 candidates; a multi-rank run also times the strong split (4096 over the ranks) and reports it beside
+the value as "strong_scaling".
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg1..cfg5] [--dtype ...]
   torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+`--gpus N` without torchrun starts the N rank processes itself (launch_ranks); under torchrun --gpus must
+equal WORLD_SIZE. `--exchange gloo` rehearses the multi-rank bench with every rank on cuda:0.
 
 The other BASELINE configs are selectable with --workload (their lines are kept under profiles/):
 cfg1 (the reference's CPU-sized case), cfg3 (pendulum, 1D U-Net, CFG-DDIM 100 steps), cfg4 (cart-pole
@@ -220,13 +224,72 @@ def panda(args):
     print(json.dumps(out), flush=True)
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, exchange, argv):
+    """`bench.py --gpus N` (N > 1) outside torchrun: this parent makes no GPU call (torch.cuda.device_count() does
+    not initialise the GPU on this image) and runs N fresh child processes of this same command line, one per GPU,
+    each with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in its environment - the env rendezvous
+    torchrun would give them. Rank 0's stdout (the JSON line) is relayed; the other ranks' stdout goes to stderr.
+    The first rank that fails takes the others down and the parent exits with its status."""
+    import subprocess
+    import threading
+    if exchange == "rccl":
+        visible = torch.cuda.device_count()
+        if visible < n:
+            raise SystemExit(f"bench.py --gpus {n}: only {visible} GPU(s) visible; refusing to time {n} ranks on "
+                             f"fewer GPUs (--exchange gloo runs every rank on cuda:0 as a rehearsal)")
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr))
+    lines = []
+    reader = threading.Thread(target=lambda: lines.extend(procs[0].stdout), daemon=True)
+    reader.start()
+    failed = None
+    while failed is None and any(p.poll() is None for p in procs):
+        failed = next((r for r, p in enumerate(procs) if p.poll() not in (None, 0)), None)
+        time.sleep(0.2)
+    if failed is None:
+        failed = next((r for r, p in enumerate(procs) if p.returncode != 0), None)
+    if failed is not None:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for p in procs:
+        p.wait()
+    reader.join(timeout=10)
+    for ln in lines:
+        sys.stdout.write(ln.decode(errors="replace"))
+    sys.stdout.flush()
+    if failed is not None:
+        raise SystemExit(f"bench.py: rank {failed} of {n} exited with status {procs[failed].returncode}")
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: WORLD_SIZE under torchrun, else 1); N > 1 without torchrun "
+                         "starts the N rank processes itself")
+    ap.add_argument("--exchange", default="rccl", choices=["rccl", "gloo"],
+                    help="rccl: one GPU per rank, the per-step exchange inside libmpcd.so over RCCL (the product); "
+                         "gloo: every rank on cuda:0, the exchange through torch.distributed over gloo (a one-GPU "
+                         "rehearsal of the multi-rank bench)")
     ap.add_argument("--steps", type=int, default=None, help="timed control steps (default 50; U-Net configs 5)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed control steps (default 20: the shader clock settles over the first dozen launches; U-Net configs 2, the first one runs the tiling autotune)")
-    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
-                    help="strong (SURVEY §8d: fixed B_total split over the ranks) or weak (B per rank)")
+    ap.add_argument("--scaling", default=None, choices=["strong", "weak"],
+                    help="weak: every GPU runs the workload's B candidates and the units all ranks process add up "
+                         "(a multi-rank run also times the strong split beside it); strong: B_total split over the "
+                         "ranks (SURVEY §8d). Default: strong for the configs BASELINE names as sharded across 8 "
+                         "GPUs (cfg4, cfg5), weak otherwise")
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS) + ["panda"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-shard-probe", action="store_true", help="skip the strong-scaling shard probes (kernel traces)")
@@ -234,6 +297,15 @@ def main():
     ap.add_argument("--dtype", default=None, choices=["f32", "f32x3", "f16"],
                     help="GEMM numerics: exact fp32 MFMA, fp32-accurate split-bf16 MFMA, fp16 operands (U-Net)")
     args = ap.parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if (args.gpus or 1) > 1:
+            if args.workload == "panda":
+                raise SystemExit("--workload panda is a one-GPU latency bench")
+            return launch_ranks(args.gpus, args.exchange, sys.argv[1:])
+    elif args.gpus is not None and args.gpus != int(env_world):
+        raise SystemExit(f"bench.py --gpus {args.gpus} under a launcher with WORLD_SIZE={env_world}: the rank count "
+                         "and --gpus must agree")
     if args.workload == "panda":
         return panda(args)
     cfg = dict(WORKLOADS[args.workload])
@@ -242,15 +314,25 @@ def main():
     steps = args.steps if args.steps is not None else (5 if unet else 50)
     warmup = args.warmup if args.warmup is not None else (2 if unet else 20)
     rank, world, local = _rank_env()
+    gloo = world > 1 and args.exchange == "gloo"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if gloo:  # rehearsal: every rank on cuda:0, torch.distributed over gloo
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo")
+        else:
+            visible = torch.cuda.device_count()
+            if local >= visible:
+                raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {visible} GPU(s) visible")
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
+        if torch.cuda.device_count() < 1:
+            raise SystemExit("bench.py: no GPU visible")
         torch.cuda.set_device(0)
-    if args.scaling == "strong":
-        if cfg["B"] % world:
-            raise SystemExit(f"{args.workload}: {cfg['B']} candidates do not split over {world} ranks")
+    if cfg["B"] % world:
+        raise SystemExit(f"{args.workload}: {cfg['B']} candidates do not split over {world} ranks")
+    if (args.scaling or ("strong" if cfg["split"] else "weak")) == "strong":
         b_local, scaling = cfg["B"] // world, "strong"
     else:
         b_local, scaling = cfg["B"], "weak"
@@ -266,38 +348,50 @@ def main():
     rng = np.random.default_rng(1)
     x0s = rng.uniform(-1, 1, (warmup + steps, system.n_x))
     n_evals = plan.n_denoise_steps(cfg["sampler"], 0, cfg["ddim_steps"])  # CFG steps (2 forwards each)
-    # the per-step exchange runs inside libmpcd.so (RCCL communicator of the planner's context)
-    comm = D.NativeComm(plan) if world > 1 else None
+    # rccl: the per-step exchange runs inside libmpcd.so (RCCL communicator of the planner's context);
+    # gloo rehearsal: the composed step, exchange through torch.distributed (distributed.select)
+    comm = D.NativeComm(plan) if world > 1 and not gloo else None
 
-    def step(i):  # one mpcd_mpc_step call: sample, clip flag, rollout/cost, select, one D2H copy
-        return plan.mpc_step(x0s[i], system, b_local, w=0.01, sample_fn=cfg["sampler"], ddim_steps=cfg["ddim_steps"],
+    def step(i, b):  # one mpc_step (rccl / one rank: one mpcd_mpc_step call) of b candidates on this rank
+        return plan.mpc_step(x0s[i], system, b, w=0.01, sample_fn=cfg["sampler"], ddim_steps=cfg["ddim_steps"],
                              seed=2 + i, comm=comm)
 
-    for i in range(warmup):
-        step(i)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    kernel_ms = []
-    t0 = time.perf_counter()
-    for i in range(steps):
-        r = step(warmup + i)
-        kernel_ms.append(plan.last_sample_ms())
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed, float(np.mean(kernel_ms))], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kms = float(t[0]), float(t[1])
-    else:
-        kms = float(np.mean(kernel_ms))
+    def timed(b):
+        """warmup + steps control steps of b candidates per rank between barriers; (wall s, mean kernel ms,
+        last result), both maxima over ranks"""
+        for i in range(warmup):
+            step(i, b)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        kernel_ms = []
+        t0 = time.perf_counter()
+        for i in range(steps):
+            res = step(warmup + i, b)
+            kernel_ms.append(plan.last_sample_ms())
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el, float(np.mean(kernel_ms))], dtype=torch.float64, device="cpu" if gloo else "cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t[0]), float(t[1]), res
+        return el, float(np.mean(kernel_ms)), res
+
+    elapsed, kms, r = timed(b_local)
+    # a weak-scaling multi-rank run also times the strong split (the workload's B over the ranks) in the same job
+    strong = None
+    if world > 1 and scaling == "weak":
+        el_s, kms_s, r_s = timed(cfg["B"] // world)
+        strong = {"candidates_total": cfg["B"], "candidates_per_gpu": cfg["B"] // world, "steps": steps,
+                  "value": cfg["B"] * steps / el_s, "ms_per_step": 1e3 * el_s / steps, "kernel_ms": kms_s,
+                  "best_cost_last_step": r_s.best_cost}
 
     # strong scaling: the shard each of P = 2, 4, 8 GPUs gets (B_total / P candidates), measured here on one GPU;
     # (ms_per_step at B_total) / (ms_per_step at B_total / P) is the compute-only P-GPU speedup bound
     shard_probe = []
-    if world == 1 and scaling == "strong" and not args.no_shard_probe:
+    if world == 1 and not args.no_shard_probe:
         ms_full = 1e3 * elapsed / steps
         for div in (2, 4, 8):
             if cfg["B"] % div:
@@ -330,18 +424,18 @@ def main():
             else:
                 r_, w_ = lay.split("x")
                 kname = "mlp_x3_kernel<%d,DDPM_CFG,ctx,%s,%s>" % (cfg["H"] * cfg["d"], r_, w_)
-            timed = f"{kname}: the whole denoising loop in one persistent launch (HIP events on the call's stream)"
+            timed_desc = f"{kname}: the whole denoising loop in one persistent launch (HIP events on the call's stream)"
         else:
             form = plan.unet_form(cfg["sampler"])
             if form["fused"]:
                 kname = "unet_fused_kernel<%d,%d,%d,%d>" % (form["planes"], form["rows_per_workgroup"], cfg["H"],
                                                             form["waves_per_workgroup"])
-                timed = (f"one mpcd_sample call: {n_evals} {kname} launches (per denoise step the whole noise net "
+                timed_desc = (f"one mpcd_sample call: {n_evals} {kname} launches (per denoise step the whole noise net "
                          "for both CFG branches + the update, activations in LDS) + the x_T / chain-maxima kernels "
                          "(HIP events on the call's stream); the fused launches are >99% of it (profiles/)")
             else:
                 kname = "conv_mx_kernel<kind,planes,NN,NC> family" if dtype != "f32" else "conv_kernel family"
-                timed = ("one mpcd_sample call: every U-Net conv launch of the loop + the per-step update kernels "
+                timed_desc = ("one mpcd_sample call: every U-Net conv launch of the loop + the per-step update kernels "
                          "(HIP events on the call's stream); the convs are >99% of it (profiles/)")
         if dtype == "f32x3":
             mac_exec = cfg["mac_row"] if cfg["mac_row"] else cfg["mac"]
@@ -394,10 +488,16 @@ def main():
                        "horizon": cfg["H"], "action_dim": cfg["d"], "context_dim": cfg["C"], "denoise_steps": n_evals,
                        "sampler": f"{'CFG-DDIM' if cfg['sampler'] == 'ddim_cfg' else 'CFG-DDPM'} w=0.01",
                        "schedule": cfg["schedule"], "noise_net": cfg["net"], "parallelism": f"dp{world}",
+                       "exchange": ("none" if world == 1 else "torch.distributed gloo, every rank on cuda:0 "
+                                    "(rehearsal)" if gloo else "RCCL inside libmpcd.so (cost all-gather + winner "
+                                    "all-reduce), one GPU per rank"),
                        "gemm": gemm},
-            "roofline": dict(roof, traffic=traffic, kernel_ms=kms, timed=timed),
+            "roofline": dict(roof, traffic=traffic, kernel_ms=kms, timed=timed_desc),
             "best_cost_last_step": r.best_cost,
         }
+        if strong is not None:
+            out["strong_scaling"] = dict(strong, note="the same job's strong split: the workload's B candidates "
+                                                      "over the ranks, timed like value (max over ranks)")
         if shard_probe:
             out["strong_shard_probe"] = {
                 "note": "one GPU running the B_total/P-candidate shard each of P GPUs gets under strong scaling "

@@ -52,7 +52,8 @@ def build(force=False, verbose=False, variant=None, defines=()):
     if variant:
         out = os.path.join(PKG, f"libmpcd_{variant}.so")
         obj = OBJ + "_" + variant
-        flags += [f"-D{d}" for d in defines]
+        # MPCD_VARIANT: the wrong-result timing switches of the kernels compile only in such a build
+        flags += ["-DMPCD_VARIANT"] + [f"-D{d}" for d in defines]
         # experiment builds only: MPCD_DROP_FLAGS / MPCD_EXTRA_FLAGS (space separated) edit the compile line
         drop = os.environ.get("MPCD_DROP_FLAGS", "").split()
         for f in drop:

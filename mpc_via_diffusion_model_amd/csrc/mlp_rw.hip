@@ -94,6 +94,12 @@ MPCD_DEV f32x4 mfma_agpr1(const u32x4 &w, const u32x4 &x, f32x4 acc)
 #ifndef MPCD_RW_EXP_NOLASTEPI
 #define MPCD_RW_EXP_NOLASTEPI 0
 #endif
+#ifndef MPCD_RW_EXP_BAR2
+#define MPCD_RW_EXP_BAR2 0
+#endif
+#if !defined(MPCD_VARIANT) && (MPCD_RW_EXP_NOLASTEPI || MPCD_RW_EXP_BAR2 || defined(MPCD_PROF_FINAL_MFMA_ONLY))
+#error "wrong-result timing switches build only as an experiment variant (build.py variant: -DMPCD_VARIANT)"
+#endif
 
 template <int D0, int SMODE, bool CTX, int R>
 struct MlpRw {

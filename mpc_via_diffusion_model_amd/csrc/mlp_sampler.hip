@@ -20,6 +20,9 @@
 
 #include "internal.h"
 #include "mlp_common.h"
+#if !defined(MPCD_VARIANT) && (defined(MPCD_DIAG_NOMFMA) || defined(MPCD_DIAG_NOMISH))
+#error "wrong-result timing diagnostics build only as an experiment variant (build.py variant: -DMPCD_VARIANT)"
+#endif
 
 namespace {
 using namespace mlpc;

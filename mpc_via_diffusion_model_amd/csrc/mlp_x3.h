@@ -51,6 +51,9 @@ constexpr int ROWS_MAX = 32;
 #ifndef MPCD_X3_EXP_NOPL2
 #define MPCD_X3_EXP_NOPL2 0
 #endif
+#if !defined(MPCD_VARIANT) && (MPCD_X3_WF32 || MPCD_X3_EXP_NOPL2)
+#error "unfinished / wrong-result experiment switches build only as a variant (build.py variant: -DMPCD_VARIANT)"
+#endif
 constexpr int THREADS = 64 * MPCD_X3_WAVES;
 constexpr int WAVES = THREADS / 64;
 enum { SPLIT = 0, PAIRED = 1, WIDE8 = 2, PAIR8 = 3 };

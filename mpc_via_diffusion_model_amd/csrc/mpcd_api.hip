@@ -818,8 +818,6 @@ int mpcd_unet_form(mpcd_ctx *c, int32_t sampler, int32_t out[4])
 int mpcd_mlp_layout(int64_t batch, int32_t cfg_masked, int32_t *layout_out)
 {
     if (batch < 1 || !layout_out) return fail(MPCD_EINVAL, "mpcd_mlp_layout: bad arguments");
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
     *layout_out = mlp_x3_layout_of(batch, cfg_masked ? 2 : 1);
     return MPCD_OK;
 }

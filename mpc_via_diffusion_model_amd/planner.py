@@ -209,7 +209,7 @@ class DiffusionMPC:
         """system.desc() (a ctypes struct), rebuilt only when the system's fields change: a control loop calls
         mpc_step with the same system every step."""
         key = (system.system, system.cost_kind, system.n_x, system.n_u, tuple(system.params), tuple(system.Q),
-               tuple(system.R), tuple(system.P), tuple(system.x_ref))
+               tuple(system.R), tuple(system.P), tuple(system.x_ref or ()))
         c = getattr(self, "_desc_cache", None)
         if c is None or c[0] != key:
             c = self._desc_cache = (key, system.desc())
@@ -339,7 +339,8 @@ class DiffusionMPC:
     def mlp_layout(self, n_samples):
         """The MLP sampler layout ("32x8", "16x8", "16x4", "rw32", "rw16") a sample call of n_samples runs."""
         out = ctypes.c_int32()
-        N.check(self._lib.mpcd_mlp_layout(int(n_samples), int(self.spec.cfg), ctypes.byref(out)), "mpcd_mlp_layout")
+        with torch.cuda.device(self.device):  # the library decides on the current device's CU count
+            N.check(self._lib.mpcd_mlp_layout(int(n_samples), int(self.spec.cfg), ctypes.byref(out)), "mpcd_mlp_layout")
         return {v: k for k, v in MLP_LAYOUTS.items()}[out.value]
 
     def last_sample_ms(self):

@@ -4,7 +4,11 @@ gloo group, as a process per GPU would with RCCL) on its shard of the cfg2 candi
 unique-id hand-off (mpcd_comm_unique_id on rank 0, broadcast over the group) without the RCCL init, which
 needs a GPU per rank. Writes its results to <out>.rank<r>.npz.
 
-    python tests/_mp_mpc_step_worker.py RANK WORLD PORT OUT B_TOTAL"""
+    python tests/_mp_mpc_step_worker.py RANK WORLD PORT OUT B_TOTAL [MODE]
+
+MODE "rccl": the product path instead - NativeComm (the unique id over the gloo group, then mpcd_comm_init: an RCCL
+communicator of WORLD ranks, here all on cuda:0) and the native mpc_step whose exchange runs inside libmpcd.so. If
+RCCL refuses the communicator (several ranks on one device) the worker prints RCCL_INIT_REFUSED and exits 3."""
 import ctypes
 import os
 import sys
@@ -25,6 +29,7 @@ H, d, C, NSTEPS, SEED = 32, 2, 4, 100, 2
 
 def main():
     rank, world, port, out, b_total = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], int(sys.argv[5])
+    mode = sys.argv[6] if len(sys.argv) > 6 else "gloo"
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -32,6 +37,18 @@ def main():
         plan = DiffusionMPC(NetSpec("mlp", state_dim=d, horizon=H, context_dim=C, dtype="f32x3"), net.state_dict(),
                             variance_schedule="exponential", n_diffusion_steps=NSTEPS)
         x0 = np.random.default_rng(1).uniform(-1, 1, C)
+        if mode == "rccl":
+            from mpc_via_diffusion_model_amd import distributed as D
+            try:
+                comm = D.NativeComm(plan)
+            except N.MpcdError as e:
+                print(f"RCCL_INIT_REFUSED: {e}", flush=True)
+                sys.exit(3)
+            res = plan.mpc_step(x0, systems.get("double_int2d"), b_total // world, w=0.01, seed=SEED, comm=comm)
+            torch.cuda.synchronize()
+            np.savez(f"{out}.rank{rank}.npz", best_index=res.best_index, best_cost=res.best_cost, u_best=res.u_best,
+                     u0=res.u0, costs=res.costs.cpu().numpy(), uid=np.zeros(1, dtype=np.uint8) + 1)
+            return
         res = plan.mpc_step(x0, systems.get("double_int2d"), b_total // world, w=0.01, seed=SEED)
         torch.cuda.synchronize()
         # NativeComm's id plumbing (distributed.py NativeComm.__init__) up to, not including, mpcd_comm_init

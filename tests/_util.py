@@ -28,7 +28,7 @@ def assert_traj_close(got, ref, rel=REL_TRAJ, abs_elem=ABS_ELEM, what="", spread
     """per trajectory ||d||_2/||ref||_2 <= rel and elementwise |d| <= abs_elem*max(|ref|, 1).
     spread: the oracle's own elementwise spread of an ill-conditioned chain (oracle_sensitivity); the elementwise
     bar is then max(abs_elem, SPREAD_X * spread), and the measured error / spread ratio is appended to the file
-    $MPCD_SPREAD_LOG names (profiles/r4_spread_ratios.tsv is the GPU run's record)."""
+    $MPCD_SPREAD_LOG names (profiles/r5_spread_ratios.tsv is the GPU run's record)."""
     got = got.detach().cpu().double().numpy()
     ref = ref.detach().cpu().double().numpy()
     assert got.shape == ref.shape, (got.shape, ref.shape)
@@ -42,42 +42,79 @@ def assert_traj_close(got, ref, rel=REL_TRAJ, abs_elem=ABS_ELEM, what="", spread
         log = os.environ.get("MPCD_SPREAD_LOG")
         if log and spread > 0:
             with open(log, "a") as f:
-                f.write(f"{what}\t{el.max():.4e}\t{spread:.4e}\t{el.max() / max(spread, 1e-30):.3f}\t{tr.max():.4e}\n")
+                jit = getattr(spread, "jitter", None)
+                jcols = f"\t{jit:.4e}\t{el.max() / max(jit, 1e-30):.3f}" if jit else "\t-\t-"
+                f.write(f"{what}\t{el.max():.4e}\t{float(spread):.4e}\t{el.max() / max(spread, 1e-30):.3f}\t{tr.max():.4e}"
+                        f"{jcols}\n")
     assert tr.max() <= rel, f"{what}: worst trajectory rel err {tr.max():.3e} (> {rel})"
     assert el.max() <= abs_elem, f"{what}: worst element err {el.max():.3e} (> {abs_elem})"
     return tr.max(), el.max()
 
 
 # elementwise bar of an ill-conditioned chain (unclamped DDIM, the trained 30-step Panda / LMPC chains): this multiple
-# of the oracle's own spread. Another fp32-accurate implementation (split-bf16 GEMMs, its own reduction orders)
-# lands a small multiple of that one-perturbation sample away: measured at most 2.89x over every such test of the GPU
-# suite (profiles/r4_spread_ratios.tsv: MLP DDIM 2.89, MLP CFG-DDIM 2.36, fused U-Net CFG-DDIM 2.11, Panda 2.02,
-# LMPC 1.81), so the bar is that maximum rounded up; the trajectory bar (1e-4 relative) is not relaxed.
-SPREAD_X = 3
+# of the oracle's own spread when its layers round from fp64 (oracle_sensitivity). Another fp32-accurate implementation
+# (split-bf16 GEMMs, its own reduction orders) lands a small multiple of that spread away: at most 2.89x in round 4
+# (profiles/r4_spread_ratios.tsv: MLP DDIM 2.89, MLP CFG-DDIM 2.36, fused U-Net CFG-DDIM 2.11, Panda 2.02, LMPC 1.81;
+# this round's record: profiles/r5_spread_ratios.tsv). 4 keeps >= 25 % headroom over that maximum. The oracle's own
+# spread under four seeded random half-ulp roundings of every layer is larger still (up to 34x the fp64 spread on
+# the MLP DDIM chain), so the bar stays anchored on the tightest perturbation; the trajectory bar (1e-4) is not relaxed.
+SPREAD_X = 4
+SENSITIVITY_SEEDS = (1, 2, 3, 4)
 
 
-def oracle_sensitivity(run):
-    """Elementwise spread of the oracle itself when every Linear/Conv/GroupNorm rounds from fp64 instead of
-    fp32 (a 1-ulp-level perturbation). Unclamped DDIM is ill-conditioned (x0 = a*x - b*eps with a, b up to
-    2.6e6 at N=100), so its elementwise parity bar is this spread, not 1e-4; the trajectory bar stays."""
+class Spread(float):
+    """The fp64-perturbation spread (the bar's anchor); .jitter = the largest spread over the seeded random
+    roundings, when recorded (MPCD_SPREAD_LOG set), else None."""
+    jitter = None
+
+
+def oracle_sensitivity(run, seeds=SENSITIVITY_SEEDS):
+    """Elementwise spread of the oracle itself when every Linear / Conv / GroupNorm rounds from fp64 instead of fp32
+    (a 1-ulp-level perturbation). Unclamped DDIM is ill-conditioned (x0 = a*x - b*eps with a, b up to 2.6e6 at N=100),
+    so its elementwise parity bar is this spread, not 1e-4; the trajectory bar stays. With MPCD_SPREAD_LOG set (the
+    recorded GPU runs) the spread under each seeded random half-ulp rounding of every layer output (x (1 + 2^-24 u),
+    u ~ U(-1, 1) per element) is measured too, and its maximum logged beside the bar's anchor."""
     import torch.nn as nn
     import torch.nn.functional as F
     ref = run()
     saved = (nn.Linear.forward, nn.Conv1d.forward, nn.ConvTranspose1d.forward, nn.GroupNorm.forward)
-    nn.Linear.forward = lambda self, x: F.linear(x.double(), self.weight.double(), self.bias.double()).float()
-    nn.Conv1d.forward = lambda self, x: F.conv1d(x.double(), self.weight.double(), self.bias.double(), self.stride,
-                                                 self.padding).float()
-    nn.ConvTranspose1d.forward = lambda self, x: F.conv_transpose1d(x.double(), self.weight.double(),
-                                                                    self.bias.double(), self.stride,
-                                                                    self.padding).float()
-    nn.GroupNorm.forward = lambda self, x: F.group_norm(x.double(), self.num_groups, self.weight.double(),
-                                                        self.bias.double(), self.eps).float()
-    try:
-        pert = run()
-    finally:
-        nn.Linear.forward, nn.Conv1d.forward, nn.ConvTranspose1d.forward, nn.GroupNorm.forward = saved
-    r, p = ref.double(), pert.double()
-    return ref, float(((p - r).abs() / r.abs().clamp_min(1.0)).max())
+
+    def with_fp64():
+        nn.Linear.forward = lambda self, x: F.linear(x.double(), self.weight.double(), self.bias.double()).float()
+        nn.Conv1d.forward = lambda self, x: F.conv1d(x.double(), self.weight.double(), self.bias.double(),
+                                                     self.stride, self.padding).float()
+        nn.ConvTranspose1d.forward = lambda self, x: F.conv_transpose1d(x.double(), self.weight.double(),
+                                                                        self.bias.double(), self.stride,
+                                                                        self.padding).float()
+        nn.GroupNorm.forward = lambda self, x: F.group_norm(x.double(), self.num_groups, self.weight.double(),
+                                                            self.bias.double(), self.eps).float()
+
+    def with_jitter(seed):
+        g = torch.Generator().manual_seed(seed)
+
+        def jitter(fwd):
+            def f(self, x):
+                y = fwd(self, x)
+                u = torch.rand(y.shape, generator=g, dtype=torch.float64) * 2 - 1
+                return (y.double() * (1 + u * 2.0 ** -24)).float()
+            return f
+        nn.Linear.forward, nn.Conv1d.forward, nn.ConvTranspose1d.forward, nn.GroupNorm.forward = (
+            jitter(fw) for fw in saved)
+
+    r = ref.double()
+
+    def spread_of(perturb):
+        perturb()
+        try:
+            p = run().double()
+        finally:
+            nn.Linear.forward, nn.Conv1d.forward, nn.ConvTranspose1d.forward, nn.GroupNorm.forward = saved
+        return float(((p - r).abs() / r.abs().clamp_min(1.0)).max())
+
+    out = Spread(spread_of(with_fp64))
+    if os.environ.get("MPCD_SPREAD_LOG") and seeds:
+        out.jitter = max(spread_of(lambda s=s: with_jitter(s)) for s in seeds)
+    return ref, out
 
 
 def unnormalize_np(x, mn, mx):

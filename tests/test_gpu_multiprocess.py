@@ -29,25 +29,24 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.timeout(240)
-def test_two_processes_on_one_gpu_match_one_process(tmp_path):
-    world, b_total = 2, 4096
+def _run_ranks(tmp_path, world, b_total, mode, timeout=200):
     port, out = str(_free_port()), str(tmp_path / "mp")
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "_mp_mpc_step_worker.py"), str(r), str(world), port,
-                               out, str(b_total)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                               out, str(b_total), mode], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
              for r in range(world)]
     logs = []
     try:
         for p in procs:
-            logs.append(p.communicate(timeout=200)[0].decode(errors="replace"))
+            logs.append(p.communicate(timeout=timeout)[0].decode(errors="replace"))
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    for r, p in enumerate(procs):
-        assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{logs[r][-3000:]}"
+    return procs, logs, out
 
+
+def _reference(b_total):
     H, d, C = 32, 2, 4
     net = make_mlp(d, H, C, seed=0)
     plan = DiffusionMPC(NetSpec("mlp", state_dim=d, horizon=H, context_dim=C, dtype="f32x3"), net.state_dict(),
@@ -55,7 +54,16 @@ def test_two_processes_on_one_gpu_match_one_process(tmp_path):
     x0 = np.random.default_rng(1).uniform(-1, 1, C)
     ref = plan.mpc_step(x0, systems.get("double_int2d"), b_total, w=0.01, seed=2)
     torch.cuda.synchronize()
-    ref_costs = ref.costs.cpu().numpy()
+    return ref, ref.costs.cpu().numpy()
+
+
+@pytest.mark.timeout(240)
+def test_two_processes_on_one_gpu_match_one_process(tmp_path):
+    world, b_total = 2, 4096
+    procs, logs, out = _run_ranks(tmp_path, world, b_total, "gloo")
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{logs[r][-3000:]}"
+    ref, ref_costs = _reference(b_total)
     uids = []
     for r in range(world):
         z = np.load(f"{out}.rank{r}.npz")
@@ -67,3 +75,24 @@ def test_two_processes_on_one_gpu_match_one_process(tmp_path):
     assert uids[0].any() and all(np.array_equal(u, uids[0]) for u in uids), "NativeComm unique id not shared"
     print(f"2 processes x {b_total // world} candidates on cuda:0 = one process x {b_total}: winner {ref.best_index}, "
           f"cost {ref.best_cost:.6f}")
+
+
+@pytest.mark.timeout(240)
+def test_two_processes_rccl_exchange_on_one_gpu(tmp_path):
+    """The product exchange (NativeComm: RCCL communicator inside libmpcd.so, native mpcd_mpc_step) with two ranks on
+    the one device this box has. RCCL may refuse a communicator with two ranks on one GPU: then this is skipped and the
+    driver's multi-GPU run is the first RCCL run with more than one rank."""
+    world, b_total = 2, 4096
+    procs, logs, out = _run_ranks(tmp_path, world, b_total, "rccl", timeout=150)
+    if any(p.returncode == 3 for p in procs):
+        msg = next(ln for lg in logs for ln in lg.splitlines() if "RCCL_INIT_REFUSED" in ln)
+        pytest.skip(f"RCCL refuses two ranks on one device: {msg[:300]}")
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{logs[r][-3000:]}"
+    ref, ref_costs = _reference(b_total)
+    for r in range(world):
+        z = np.load(f"{out}.rank{r}.npz")
+        np.testing.assert_array_equal(z["costs"], ref_costs)
+        assert int(z["best_index"]) == ref.best_index and float(z["best_cost"]) == ref.best_cost, r
+        np.testing.assert_array_equal(z["u_best"], ref.u_best)
+    print(f"RCCL, 2 ranks on cuda:0: winner {ref.best_index} = one process")

@@ -41,12 +41,13 @@ def _disassemble(tmp_path):
 
 
 def test_every_kernel_keeps_packed_reads_of_transcendentals_two_wait_states_away(tmp_path):
-    """Every kernel of the shipped code object: the MLP samplers (mlp_x3_kernel is the cfg2 headline kernel), the
-    layer-by-layer and fused U-Nets, the prologues, the rollout and the training kernels."""
+    """Every kernel of the shipped code object: the MLP samplers (mlp_rw_kernel is the cfg2 headline kernel; the
+    streaming mlp_x3_kernel and the exact-fp32 mlp_sample_kernel), the layer-by-layer and fused U-Nets, the prologues,
+    the rollout and the training kernels."""
     import trans_hazard as th
     sites = th.scan(_disassemble(tmp_path))
     kernels = {s[0] for s in sites if s[0]}
-    for k in ("unet_fused_kernel", "conv_mx_kernel", "mlp_x3_kernel", "mlp_sample_kernel"):
+    for k in ("unet_fused_kernel", "conv_mx_kernel", "mlp_rw_kernel", "mlp_x3_kernel", "mlp_sample_kernel"):
         assert any(k in n for n in kernels), f"{k} not found in the code object"
     packed = [s for s in sites if s[4]]
     close = [s for s in packed if s[3] < 2]
@@ -68,18 +69,33 @@ def test_every_mfma_source_two_wait_states_after_a_valu_write(tmp_path):
 
 
 def test_asm_mfma_results_wait_before_valu_reads(tmp_path):
-    """The other direction for the inline-asm MFMAs (AGPR operands): a VALU op may read an MFMA result only 8
-    wait states after it - what hipcc inserts after the builtin v_mfma_f32_16x16x32_bf16 (checked here too),
-    and what the asm statements of csrc/mlp_rw.hip write themselves."""
+    """The other direction for the inline-asm MFMAs (AGPR operands): a VALU op may read an MFMA result - or overwrite
+    it (write after write; in these in-place chains also the write after the in-flight MFMA's srcC read) - only as
+    many wait states after it as hipcc leaves after the builtin v_mfma_f32_16x16x32_bf16 (its minimum over the whole
+    library is the toolchain's requirement: 8 today, which the asm statements of csrc/mlp_rw.hip write out). If a
+    toolchain raises that requirement, the asm waits fall under it and this fails."""
     import mfma_hazard as mh
-    reads = mh.result_reads(_disassemble(tmp_path))
-    bf16 = [r for r in reads if r[1].startswith("v_mfma_f32_16x16x32_bf16")]
+    acc = mh.result_reads(_disassemble(tmp_path))
+    bf16 = [r for r in acc if r[1].startswith("v_mfma_f32_16x16x32_bf16")]
     builtin = [r for r in bf16 if ", a[" not in r[1]]
     asm = [r for r in bf16 if ", a[" in r[1]]
     assert builtin and asm, "expected both builtin and AGPR-operand bf16 MFMAs"
-    assert min(r[3] for r in builtin) >= 8, "hipcc's own wait after the bf16 MFMA changed: revisit mlp_rw.hip"
-    close = [r for r in asm if r[3] < 8]
-    assert not close, f"{len(close)} VALU reads of an asm MFMA result under 8 wait states: {close[:3]}"
+    req = min(r[3] for r in builtin if r[4] == "read")
+    assert req == 8, f"hipcc's own wait after the bf16 MFMA is now {req} (was 8): revisit mlp_rw.hip's s_nop 7"
+    close = [r for r in asm if r[3] < req]
+    assert not close, (f"{len(close)} VALU accesses of an asm MFMA result under {req} wait states "
+                       f"(reads {sum(r[4] == 'read' for r in close)}, writes {sum(r[4] == 'write' for r in close)}): "
+                       f"{close[:3]}")
+
+
+def test_result_scan_reports_close_reads_and_writes():
+    import mfma_hazard as mh
+    asm = ["_Z1kv:", "  v_mfma_f32_16x16x32_bf16 v[28:31], a[20:23], v[0:3], v[28:31]", "  s_nop 3",
+           "  v_mov_b32_e32 v29, v33",
+           "  v_mfma_f32_16x16x32_bf16 v[8:11], a[20:23], v[0:3], v[8:11]", "  s_nop 1",
+           "  v_add_f32_e32 v40, v9, v9"]
+    got = [(r[2].split()[0], r[3], r[4]) for r in mh.result_reads(asm)]
+    assert got == [("v_mov_b32_e32", 4, "write"), ("v_add_f32_e32", 2, "read")], got
 
 
 def test_mfma_scan_finds_a_close_valu_write():

@@ -80,8 +80,11 @@ def scan(lines, need=2):
 
 
 def result_reads(lines, kernel_filter=None):
-    """[(kernel, mfma inst, first VALU reader of its result, wait states)] for every v_mfma_*: the walk forward
-    stops at the first VALU op that reads the destination (or overwrites it), a label or a branch."""
+    """[(kernel, mfma inst, first VALU access of its result, wait states, kind)] for every v_mfma_*: the walk
+    forward stops at the first VALU op that reads the destination (kind "read") or overwrites it without reading
+    it (kind "write": a write-after-write of the accumulator, which in the in-place chains of this library is also
+    the write-after-read of the in-flight MFMA's srcC), a label or a branch. A following MFMA that reads the
+    result as srcA / srcB is reported as a read; one that takes it as srcC continues the chain (forwarding)."""
     insts = instructions(lines)
     out = []
     for i, (k, t) in enumerate(insts):
@@ -102,17 +105,18 @@ def result_reads(lines, kernel_filter=None):
                 uops = up[1].split(",")
                 if up[0].startswith("v_mfma"):
                     if regs(",".join(uops[1:3])) & dst:  # read as srcA / srcB: not a forwarding case, report
-                        out.append((k, t, u, ws))
+                        out.append((k, t, u, ws, "read"))
                         break
                     if regs(uops[0]) & dst and not regs(",".join(uops[3:4])) & dst:
-                        break  # overwritten
+                        break  # overwritten by another MFMA (the matrix pipe orders its own writes)
                     if regs(",".join(uops[3:4])) & dst:
                         break  # srcC of the next MFMA (forwarding): the chain continues there
                 else:
                     if regs(",".join(uops[1:])) & dst:
-                        out.append((k, t, u, ws))
+                        out.append((k, t, u, ws, "read"))
                         break
                     if regs(uops[0]) & dst:
+                        out.append((k, t, u, ws, "write"))
                         break
             ws += 1
     return out
