@@ -294,8 +294,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-shard-probe", action="store_true", help="skip the strong-scaling shard probes (kernel traces)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--dtype", default=None, choices=["f32", "f32x3", "f16"],
-                    help="GEMM numerics: exact fp32 MFMA, fp32-accurate split-bf16 MFMA, fp16 operands (U-Net)")
+    ap.add_argument("--candidates", type=int, default=None,
+                    help="override the workload's B (profiling a shard size; the line then names the changed config)")
+    ap.add_argument("--dtype", default=None, choices=["f32", "f32x3", "f16", "f16x2"],
+                    help="GEMM numerics: exact fp32 MFMA, fp32-accurate split-bf16 MFMA, fp16 operands (U-Net), "
+                         "fp32-class two-term fp16 MFMA (MLP)")
     args = ap.parse_args()
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None:
@@ -309,6 +312,8 @@ def main():
     if args.workload == "panda":
         return panda(args)
     cfg = dict(WORKLOADS[args.workload])
+    if args.candidates:
+        cfg.update(B=args.candidates, workload=cfg["workload"] + f" [B overridden: {args.candidates}]")
     dtype = args.dtype or cfg["dtype"]
     unet = cfg["net"] == "unet"
     steps = args.steps if args.steps is not None else (5 if unet else 50)
@@ -416,14 +421,17 @@ def main():
         flops_launch = b_local * n_evals * 2 * 2 * cfg["mac"]   # survey's algorithmic count (fp32 FLOPs)
         achieved = flops_launch / (kms * 1e-3)
         if not unet:
-            lay = plan.mlp_layout(b_local) if dtype == "f32x3" else None
-            if dtype == "f32":
-                kname = "mlp_sample_kernel<%d,DDPM_CFG,ctx>" % (cfg["H"] * cfg["d"])
-            elif lay.startswith("rw"):
-                kname = "mlp_rw_kernel<%d,DDPM_CFG,ctx,%s>" % (cfg["H"] * cfg["d"], lay[2:])
+            form = plan.mlp_form(b_local, cfg["sampler"])
+            tmpl = "%d,DDPM_CFG,ctx" % (cfg["H"] * cfg["d"])
+            if form["kernel"] == "f32":
+                kname = "mlp_sample_kernel<%s>" % tmpl
+            elif form["kernel"] == "h2":
+                kname = "mlp_h2_kernel<%s,%d>" % (tmpl, form["rows_per_workgroup"])
+            elif form["layout"].startswith("rw"):
+                kname = "mlp_rw_kernel<%s,%s>" % (tmpl, form["layout"][2:])
             else:
-                r_, w_ = lay.split("x")
-                kname = "mlp_x3_kernel<%d,DDPM_CFG,ctx,%s,%s>" % (cfg["H"] * cfg["d"], r_, w_)
+                r_, w_ = form["layout"].split("x")
+                kname = "mlp_x3_kernel<%s,%s,%s>" % (tmpl, r_, w_)
             timed_desc = f"{kname}: the whole denoising loop in one persistent launch (HIP events on the call's stream)"
         else:
             form = plan.unet_form(cfg["sampler"])
@@ -437,18 +445,21 @@ def main():
                 kname = "conv_mx_kernel<kind,planes,NN,NC> family" if dtype != "f32" else "conv_kernel family"
                 timed_desc = ("one mpcd_sample call: every U-Net conv launch of the loop + the per-step update kernels "
                          "(HIP events on the call's stream); the convs are >99% of it (profiles/)")
-        if dtype == "f32x3":
+        if dtype in ("f32x3", "f16x2"):
             mac_exec = cfg["mac_row"] if cfg["mac_row"] else cfg["mac"]
-            mfma_flops = b_local * 2 * n_evals * mac_exec * 2 * 6   # six bf16 partial products per fp32 MAC
+            prods = 3 if (not unet and form["kernel"] == "h2") else 6
+            mfma_flops = b_local * 2 * n_evals * mac_exec * 2 * prods   # bf16 / fp16 partial products per fp32 MAC
             roof = {"bound": "mfma", "achieved": mfma_flops / (kms * 1e-3) / 1e12, "peak": PEAK_BF16 / 1e12,
                     "unit": "TFLOP/s", "frac": mfma_flops / (kms * 1e-3) / PEAK_BF16,
-                    "peak_note": "bf16 dense MFMA peak; the kernels compute fp32-accurate GEMMs as 3-way bf16 splits "
-                                 "(6 partial products per fp32 MAC)",
+                    "peak_note": ("fp16 dense MFMA peak (= bf16); the kernel computes fp32-class GEMMs as two fp16 terms "
+                                  "per operand (3 partial products per fp32 MAC)") if prods == 3 else
+                                 ("bf16 dense MFMA peak; the kernels compute fp32-accurate GEMMs as 3-way bf16 splits "
+                                  "(6 partial products per fp32 MAC)"),
                     # the same executed MACs at the fp32 rate (the survey's algorithmic count, flops_launch, also
                     # counts the per-candidate time / cond MLPs the kernel computes once per step)
-                    "fp32_equiv": {"achieved": mfma_flops / 6 / (kms * 1e-3) / 1e12, "peak": PEAK_FP32 / 1e12,
-                                   "frac": mfma_flops / 6 / (kms * 1e-3) / PEAK_FP32,
-                                   "flop_per_launch": mfma_flops / 6, "algorithmic_flop_per_launch": flops_launch},
+                    "fp32_equiv": {"achieved": mfma_flops / prods / (kms * 1e-3) / 1e12, "peak": PEAK_FP32 / 1e12,
+                                   "frac": mfma_flops / prods / (kms * 1e-3) / PEAK_FP32,
+                                   "flop_per_launch": mfma_flops / prods, "algorithmic_flop_per_launch": flops_launch},
                     "kernel": kname, "flop_per_launch": mfma_flops}
         elif dtype == "f16":
             roof = {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
@@ -468,6 +479,8 @@ def main():
                 traffic = pm.get("hbm_bytes_per_launch")
         gemm = {"f32": "exact fp32 MFMA (v_mfma_f32_16x16x4_f32)",
                 "f32x3": "fp32-accurate split-bf16 MFMA (3 bf16 terms per operand, 6 partial products, fp32 accumulate)",
+                "f16x2": "fp32-class two-term fp16 MFMA (hi + lo fp16 per operand, weights scaled per layer by a power of "
+                         "two; 3 partial products, fp32 accumulate) for CFG-DDPM; the f32x3 kernels otherwise",
                 "f16": "fp16 operands, fp32 accumulate (v_mfma_f32_16x16x32_f16)"}[dtype]
         out = {
             "metric": "candidate trajectories/sec (100 denoise steps, H=32)" if args.workload == "cfg2" else
@@ -481,7 +494,7 @@ def main():
             "higher_is_better": True,
             "scaling": scaling,
             "vs_baseline": None,
-            "dtype": "f16" if dtype == "f16" else "f32",
+            "dtype": "f16" if dtype == "f16" else "f32",  # f16x2 / f32x3: fp32-class results (tests/test_gpu_headline.py)
             "data": f"synthetic (random-init weights seed 0 by PyTorch's default-init rule, x0 ~ U[-1,1]^{cfg['C']}, "
                     "Philox noise)",
             "config": {"workload": cfg["workload"], "candidates_per_gpu": b_local, "candidates_total": b_local * world,

@@ -55,8 +55,14 @@ enum mpcd_net_kind {
  * MPCD_F32X3: fp32-accurate split-bf16 MFMA (MLP and U-Net): each fp32 operand = three bf16 terms, the six
  *             partial products >= 2^-16 of the leading one accumulated in fp32 (error at the level of
  *             the fp32 MFMA's). MLP: needs a context shared by all candidates (or none); a
- *             per-candidate context runs the MPCD_F32 kernel. */
-enum mpcd_dtype { MPCD_F32 = 0, MPCD_F16 = 1, MPCD_F32X3 = 2 };
+ *             per-candidate context runs the MPCD_F32 kernel.
+ * MPCD_F16X2: fp32-class two-term fp16 MFMA (MLP only, csrc/mlp_h2.hip): each fp32 operand = hi + lo (two fp16,
+ *             the weights scaled per layer by an exact power of two), three products per 32-k chunk accumulated
+ *             in fp32 (error <= 2^-22 of |w||x| per product, the order of fp32's own summation error). Used for
+ *             the CFG-DDPM sampler and the eps forward at H*d = 32 / 64 with a shared context; every other case
+ *             (unclamped DDIM, whose unbounded x leaves the fp16 range; per-candidate contexts; H*d = 128) runs
+ *             the MPCD_F32X3 kernels of the same net. */
+enum mpcd_dtype { MPCD_F32 = 0, MPCD_F16 = 1, MPCD_F32X3 = 2, MPCD_F16X2 = 3 };
 
 typedef struct {
     int32_t kind;          /* mpcd_net_kind */
@@ -345,6 +351,11 @@ int mpcd_mlp_force_layout(int32_t layout);
 /* The layout (0..4 as above) an MPCD_F32X3 MLP sample call of `batch` candidates runs on the current device
  * (cfg_masked: CFG net, two rows per candidate). */
 int mpcd_mlp_layout(int64_t batch, int32_t cfg_masked, int32_t *layout_out);
+/* Which kernel an mpcd_sample / mpcd_mpc_step call with this sampler and `batch` candidates (shared context) runs
+ * on this context's MLP, on its device: out[0] = 0 exact fp32 (mlp_sample_kernel), 1 split bf16 (mlp_x3_kernel /
+ * mlp_rw_kernel), 2 two-term fp16 (mlp_h2_kernel); out[1] = the bf16x3 layout (as mpcd_mlp_layout) or -1;
+ * out[2] = rows per workgroup (32 or 16). MPCD_EUNSUP on a U-Net context. */
+int mpcd_mlp_form(mpcd_ctx *ctx, int32_t sampler, int64_t batch, int32_t out[3]);
 /* U-Net execution form, process-wide. The whole-network form (csrc/unet_fused.hip: every conv of one denoise
  * step in ONE launch, a workgroup per few candidates, activations in LDS) covers the CFG samplers and the
  * two-branch eps of ConditionedTemporalUnet(base 32, dim_mults (1, 2, 4)) at H = 32 / 64 with the MPCD_F32X3

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MPCD_LIB") or os.path.join(_HERE, "libmpcd.so")
 
 MPCD_NET_MLP, MPCD_NET_UNET = 1, 2
-MPCD_F32, MPCD_F16, MPCD_F32X3 = 0, 1, 2
+MPCD_F32, MPCD_F16, MPCD_F32X3, MPCD_F16X2 = 0, 1, 2, 3
 MPCD_DDPM_CFG, MPCD_DDIM_CFG, MPCD_DDIM = 0, 1, 2
 MPCD_COST_CANONICAL, MPCD_COST_CALMPC = 0, 1
 MPCD_COMM_ID_BYTES = 128
@@ -106,6 +106,7 @@ EXPORTS = {
     "mpcd_unet_force_tiling": ([ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
     "mpcd_mlp_force_layout": ([ctypes.c_int32], ctypes.c_int),
     "mpcd_mlp_layout": ([ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+    "mpcd_mlp_form": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "mpcd_unet_force_path": ([ctypes.c_int32], ctypes.c_int),
     "mpcd_unet_form": ([ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "mpcd_comm_init_loopback": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64], ctypes.c_int),

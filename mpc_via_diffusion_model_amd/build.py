@@ -16,7 +16,7 @@ CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(PKG, "libmpcd.so")
 OBJ = os.path.join(PKG, "_build")
 ARCH = os.environ.get("MPCD_OFFLOAD_ARCH", "gfx950")
-SOURCES = ["mpcd_api.hip", "comm.hip", "mlp_sampler.hip", "mlp_x3.hip", "mlp_rw.hip", "cond_prologue.hip", "rollout.hip", "unet.hip", "unet_mx.hip", "unet_fused.hip", "train.hip"]
+SOURCES = ["mpcd_api.hip", "comm.hip", "mlp_sampler.hip", "mlp_x3.hip", "mlp_rw.hip", "mlp_h2.hip", "cond_prologue.hip", "rollout.hip", "unet.hip", "unet_mx.hip", "unet_fused.hip", "train.hip"]
 # -amdgpu-mfma-vgpr-form: MFMA accumulators in VGPRs (no v_accvgpr_read before every epilogue op;
 # f32 MFMA and VALU share issue on gfx950, so those moves cost MFMA time).
 # per-source additions. mlp_x3.hip: the memory-clause machine scheduler groups each layer's weight / LDS

@@ -89,6 +89,11 @@ void mlp_pack_weights_x3(int d0, const float *const *lin_w, const float *const *
 hipError_t launch_mlp_x3(int d0, int nb, const MlpSampleArgs &a, hipStream_t stream);
 // resident-weight variant (mlp_rw.hip), selected by mlp_x3's layout choice: rows = 32 or 16 per workgroup
 hipError_t launch_mlp_rw(int d0, int rows, const MlpSampleArgs &a, hipStream_t stream);
+// two-term fp16 variant (mlp_h2.hip, MPCD_F16X2): CFG-DDPM / eps at H*d 32 / 64, shared context; rows 32 or 16
+bool mlp_h2_supports(int d0, int mode);
+int mlp_packed_floats_h2(int d0);
+void mlp_pack_weights_h2(int d0, const float *const *lin_w, const float *const *lin_b, float *out);
+hipError_t launch_mlp_h2(int d0, int rows, const MlpSampleArgs &a, hipStream_t stream);
 
 // Fused selection for launch_rollout_cost (single rank): see rollout.hip SelectK
 constexpr int64_t kFuseClipMax = 16384;  // clip inputs up to this many floats are tested inside the selecting launch

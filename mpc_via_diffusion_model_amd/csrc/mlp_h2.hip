@@ -1,0 +1,765 @@
+// Persistent CFG-DDPM sampler for the MLP noise-net with fp32-class GEMMs as TWO fp16 terms
+// (MPCD_F16X2): every operand is hi + lo, hi = fp16(v), lo = fp16(v - hi), and each 32-k chunk accumulates the three
+// products lo_w*hi_x, hi_w*lo_x, hi_w*hi_x on v_mfma_f32_16x16x32_f16 into the fp32 accumulator (the dropped
+// lo_w*lo_x term and the two representation residues are each <= 2^-22 of |w||x|: the same order as fp32's own
+// rounding of a 128-term sum; tests/test_gpu_mlp_h2.py measures it against the oracle). Half the MFMAs of the
+// three-bf16-plane form (mlp_rw.hip: six products), two activation planes instead of three in LDS, and a split that
+// is two conversions and one mixed-precision FMA per pair of values instead of eleven ops.
+//
+// Range. fp16 holds |v| < 65504: the weights of each layer are scaled by an exact power of two s_l (max |w s_l| in
+// (2^9, 2^10], so lo_w stays a normal fp16), the accumulator starts from s_l * (bias or cond table) and the epilogue
+// folds 1/s_l into its constants (Mish of acc/s_l with the same ops and roundings as mish() of the unscaled value).
+// Activations are used unscaled: the CFG-DDPM chain is bounded (x0 is clamped, |x_t| stays O(1)), which is why this
+// kernel serves MODE_DDPM_CFG / MODE_DDPM_XN / MODE_EPS only (unclamped DDIM runs mlp_rw.hip); an activation beyond
+// the fp16 range turns into a non-finite sample, which the chain |x| maximum and mpcd_mpc_step report.
+//
+// Layout (one wave per SIMD, 4 waves, 512 registers each): the weights stay in registers for the whole launch -
+// Linear 2..7 (248 registers per lane: the 128-wide layers of the down path and the mid block) in AGPRs, read by
+// inline-asm MFMAs as the A operand; Linear 0, 1, 9..13 (80) in VGPRs; only Linear 8 (256 x 64) streams from L2 each
+// step, 64 KB per CU, its fragments issued in Linear 7's MFMA slots. LDS holds the activations as two fp16 planes,
+// the fp32 x, and the per-step cond tables. Same row mapping, layer order, Philox streams and denoise update as
+// mlp_rw.hip; each hidden layer is a pipeline of passes (one n-tile x one 16-row column tile) whose previous pass's
+// epilogue (Mish, split, two LDS stores) runs as micro-steps between this pass's MFMAs.
+#include <hip/hip_runtime.h>
+
+#include "mlp_x3.h"
+
+namespace {
+using namespace mlpx3;
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int H2_W = 4;           // waves per workgroup (one per SIMD)
+constexpr int H2_T = 64 * H2_W;   // threads
+constexpr int HDR = 64;           // pack header (floats): s[16], 1/s[16], log2(e)/s[16], -2/s[16]
+
+// packed floats before layer l: header, then per layer two fp16 planes of K x N (= K N floats) + N fp32 biases
+template <int D0>
+constexpr int woffh(int l)
+{
+    int o = HDR;
+    for (int i = 0; i < l; ++i) o += Arch<D0>::K[i] * Arch<D0>::N[i] + Arch<D0>::N[i];
+    return o;
+}
+
+// uniform load through the constant address space (s_load)
+MPCD_DEV float ldc(const float *p) { return *(const __attribute__((address_space(4))) float *)(uintptr_t)p; }
+
+MPCD_DEV f32x4 mfma_h(const u32x4 &a, const u32x4 &b, const f32x4 &c)
+{
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+// One product with the weight plane in an AGPR (inline asm: hipcc does not allocate builtin MFMA operands in AGPRs,
+// and its hazard pass does not see this MFMA, so the waits are written here). FIRST: 2 wait states for a VALU write
+// of the accumulator just before; LAST: 8 before any VALU op may read or overwrite the result (hipcc's wait after
+// the builtin v_mfma_f32_16x16x32_f16; tests/test_isa.py checks both rules on every MFMA of the library). Inside a
+// chain the accumulator goes MFMA to MFMA (srcC forwarding).
+template <bool FIRST, bool LAST>
+MPCD_DEV f32x4 mfma_h_agpr(const u32x4 &w, const u32x4 &x, f32x4 acc)
+{
+    if constexpr (FIRST && LAST)
+        asm("s_nop 1\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0\n\ts_nop 7" : "+v"(acc) : "a"(w), "v"(x));
+    else if constexpr (FIRST)
+        asm("s_nop 1\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(x));
+    else if constexpr (LAST)
+        asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0\n\ts_nop 7" : "+v"(acc) : "a"(w), "v"(x));
+    else
+        asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(x));
+    return acc;
+}
+
+// product m of a 32-k chunk, smallest first: lo_w * hi_x, hi_w * lo_x, hi_w * hi_x
+constexpr int wpl(int m) { return m == 0 ? 1 : 0; }
+constexpr int xpl(int m) { return m == 1 ? 1 : 0; }
+
+// two fp32 -> packed fp16 (round to nearest even: v_cvt_pk_f16_f32)
+MPCD_DEV uint32_t pk_f16(float a, float b) { return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, h16x2)); }
+// v - fp32(half h of p) in one v_fma_mix_f32 (exact: the remainder of a round-to-nearest)
+template <int HALF>
+MPCD_DEV float rem_f16(uint32_t p, float v)
+{
+    float r;
+    if constexpr (HALF == 0)
+        asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(p), "v"(v));
+    else
+        asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(p), "v"(v));
+    return r;
+}
+// 4 consecutive fp32 features -> the hi and lo fp16 planes (4 halves each)
+MPCD_DEV void split2(const f32x4 &v, u32x2 &hi, u32x2 &lo)
+{
+    const uint32_t a = pk_f16(v.x, v.y), b = pk_f16(v.z, v.w);
+    hi = u32x2{a, b};
+    lo = u32x2{pk_f16(rem_f16<0>(a, v.x), rem_f16<1>(a, v.y)), pk_f16(rem_f16<0>(b, v.z), rem_f16<1>(b, v.w))};
+}
+
+// LDS layout (bytes): as Lds3 (mlp_x3.h) with two planes per activation buffer
+template <int D0, int NB, int ROWS>
+struct Lds2 {
+    static constexpr int CPW = ROWS / NB;
+    static constexpr int RS = 272, RS2 = 528;
+    static constexpr int PL = ROWS * RS, PL2 = ROWS * RS2;
+    static constexpr int SX = D0 + 4;
+    static constexpr int T1 = 0;
+    static constexpr int S1 = T1 + 2 * PL;  // also the x planes (layer-0 input) between steps
+    static constexpr int C1 = S1 + 2 * PL;
+    static constexpr int C0 = C1 + 2 * PL;
+    static constexpr int XB = C0 + 2 * PL2;
+    static constexpr int TPC = XB + CPW * SX * 4;
+    static constexpr int TPU = TPC + COND_TOTAL * 4;
+    static constexpr int BIC = TPU + COND_TOTAL * 4;
+    static constexpr int CPS = BIC + COND_TOTAL * 4;
+    static constexpr int BI = CPS + COND_TOTAL * 4;
+    static constexpr int AMX = BI + Arch<D0>::btotal() * 4;
+    static constexpr int total = AMX + ROWS * 4;
+    static_assert(D0 * 2 + 16 <= RS, "x planes fit a 272-byte row");
+    static constexpr int in_rs(int l) { return (l == 6 || l == 8) ? RS2 : RS; }
+    static constexpr int in_pl(int l) { return (l == 6 || l == 8) ? PL2 : PL; }
+    static constexpr int out_rs(int l) { return (l == 5 || l == 7) ? RS2 : RS; }
+    static constexpr int out_pl(int l) { return (l == 5 || l == 7) ? PL2 : PL; }
+};
+
+template <int D0, int SMODE, bool CTX, int R>
+struct MlpH2 {
+    static_assert(D0 == 32 || D0 == 64, "fp16x2 MLP: H * d of 32 or 64");
+    static constexpr int NB = 2;
+    static_assert(SMODE == MODE_DDPM_CFG || SMODE == MODE_DDPM_XN || SMODE == MODE_EPS, "CFG-DDPM / eps only");
+    static constexpr bool IS_DDPM = SMODE != MODE_EPS;
+    static_assert(R == 32 || R == 16, "32 or 16 rows per workgroup");
+    static constexpr int NCT = R / 16;
+    using A = Arch<D0>;
+    using L = Lds2<D0, NB, R>;
+    static constexpr int CPW = L::CPW;
+    static constexpr int QUADS = D0 / 4;
+
+    // LDS buffer of layer l's input / output (byte offsets; the concat halves at +128 / +256 bytes of the row)
+    static constexpr int in_off(int l)
+    {
+        constexpr int t[NLAYER] = {L::S1, L::T1, L::S1, L::T1, L::C1 + 128, L::T1, L::C0 + 256, L::T1, L::C0, L::T1,
+                                   L::C1, L::T1, L::S1, L::T1};
+        return t[l];
+    }
+    static constexpr int out_off(int l)
+    {
+        constexpr int t[NLAYER] = {L::T1, L::S1, L::T1, L::C1 + 128, L::T1, L::C0 + 256, L::T1, L::C0, L::T1, L::C1,
+                                   L::T1, L::S1, L::T1, 0};
+        return t[l];
+    }
+
+    // R = 16: columns 0-7 are the context rows of candidates 0-7, 8-15 their masked rows
+    static MPCD_DEV int cand_of(int ct, int col) { return R == 16 ? (col & 7) : col; }
+    static MPCD_DEV bool masked_of(int ct, int col) { return R == 16 ? col >= 8 : ct == 1; }
+
+    // layer l's work per wave (as mlp_rw.hip): N = 32 at 32 rows: wave w -> n-tile w & 1, column tile w >> 1;
+    // otherwise wave w -> n-tiles w + 4j for every column tile
+    template <int l> static constexpr bool SPL = A::N[l] == 32 && NCT == 2;
+    template <int l> static constexpr int TL = SPL<l> ? 1 : (A::N[l] / 16 + 3) / 4;
+    template <int l> static constexpr int CL = SPL<l> ? 1 : NCT;
+    template <int l> static constexpr int KCL = A::K[l] / 32;
+    template <int l> static MPCD_DEV int nt_of(int wave, int j) { return SPL<l> ? (wave & 1) : wave + 4 * j; }
+    template <int l> static MPCD_DEV int ct_of(int wave, int c) { return SPL<l> ? (wave >> 1) : c; }
+    // where layer l's fragments live: AGPRs (asm MFMAs), VGPRs, or streamed every step (Linear 8)
+    static constexpr bool AG(int l) { return l >= 2 && l <= 7; }
+    static constexpr int NZT = TL<13>;
+
+    template <int l>
+    struct WF {
+        u32x4 v[TL<l>][KCL<l>][2];
+    };
+
+    // chunk (nt, kc, plane) of layer l at float woffh(l) + ((nt * KC + kc) * 2 + plane) * 256, 16 B per lane
+    template <int l>
+    static MPCD_DEV void load_res(WF<l> &f, const float *__restrict__ wp, int wave, int lane)
+    {
+        constexpr int KC = KCL<l>, NT = A::N[l] / 16;
+#pragma unroll
+        for (int j = 0; j < TL<l>; ++j) {
+            const int nt = min(nt_of<l>(wave, j), NT - 1);  // clamped: a wave with no tile loads and never uses
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+                for (int pl = 0; pl < 2; ++pl)
+                    f.v[j][kc][pl] = __builtin_bit_cast(u32x4, ldg4(wp + woffh<D0>(l) + ((nt * KC + kc) * 2 + pl) * 256 + lane * 4));
+        }
+    }
+    // streamed layer: fragment f (= (j * KC + kc) * 2 + plane) by one buffer load, issued as side work
+    template <int l>
+    static MPCD_DEV void load_st1(WF<l> &w, const float *__restrict__ wp, int wave, int lane16, int f)
+    {
+        constexpr int K = A::K[l], N = A::N[l], KC = K / 32, NT = N / 16;
+        const uint64_t a = (uint64_t)(wp + woffh<D0>(l));
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(K * N * 4), 0x00020000);
+        const int j = f / (KC * 2), kc = (f / 2) % KC, pl = f % 2;
+        const int nt = min(nt_of<l>(wave, j), NT - 1);
+        const int soff = __builtin_amdgcn_readfirstlane(((nt * KC + kc) * 2 + pl) * 1024);
+        w.v[j][kc][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
+    }
+    template <int l>
+    static constexpr int NFRAG = TL<l> * KCL<l> * 2;
+
+    // per-layer constants of the scaled accumulator: 1/s, log2(e)/s, -2/s
+    struct Sc {
+        float inv, c1, k2;
+    };
+    static MPCD_DEV Sc sc_of(const float *wp, int l) { return Sc{ldc(wp + 16 + l), ldc(wp + 32 + l), ldc(wp + 48 + l)}; }
+
+    // Hidden layer l as a pipeline of passes (one n-tile x one column tile: KC chunks x 3 products); the previous
+    // pass's epilogue spread as micro-steps between this pass's MFMAs, side work (loads, Philox steps) spread over
+    // the layer's MFMA slots. MM1(j, kc, m, x[2], acc) -> acc: product m of chunk kc of n-tile j.
+    template <int l, int NS, class MM1, class SIDE>
+    static MPCD_DEV void hidden(MM1 mm1, SIDE side, const Sc sc, char *lds, int wave, int lane)
+    {
+        constexpr int N = A::N[l], KC = KCL<l>, NT = N / 16, T = TL<l>, NC = CL<l>, EPI = epi_of(l);
+        constexpr int NP = T * NC, NI = NP * KC, NMF = KC * 3, TOT = NP * NMF;
+        const int col = lane & 15, q = lane >> 4;
+        constexpr bool in_shared = l == 0;  // CFG: both branches read the candidate's x
+        static_assert(T == 1 || NT % 4 == 0, "only a one-tile layer can leave a wave idle");
+        if constexpr (NT < 4 && !SPL<l>)
+            if (wave >= NT) {  // N = 32 at 16 rows: waves 2, 3 have no tile
+#pragma unroll
+                for (int k = 0; k < NS; ++k) side(k);
+                return;
+            }
+        auto jp = [](int p) { return p / NC; };
+        auto cp = [](int p) { return p % NC; };
+        auto init_of = [&](int p) {
+            const int ct = ct_of<l>(wave, cp(p));
+            const float *init = reinterpret_cast<const float *>(
+                lds + (EPI == EPI_CMISH ? (masked_of(ct, col) ? L::TPU : L::TPC) + cond_off(l / 2) * 4
+                                        : L::BI + A::boff(l) * 4));
+            return *reinterpret_cast<const f32x4 *>(init + min(nt_of<l>(wave, jp(p)), NT - 1) * 16 + 4 * q);
+        };
+        auto ldx = [&](u32x4 (&x)[2], int i) {  // step i = (pass i / KC, k-chunk i % KC)
+            const int p = i / KC, kc = i % KC, ct = ct_of<l>(wave, cp(p));
+            const int row = in_shared ? cand_of(ct, col) : ct * 16 + col;
+            const char *b = lds + in_off(l) + row * L::in_rs(l) + (kc * 32 + 8 * q) * 2;
+            x[0] = *reinterpret_cast<const u32x4 *>(b);
+            x[1] = *reinterpret_cast<const u32x4 *>(b + L::in_pl(l));
+        };
+        // epilogue micro-steps of pass p: Mish of the scaled accumulator (4 stages x 4 values, each value's dependent
+        // ops 4 steps apart; layer 12: the 4 unscaling products), then the split and the two plane stores
+        constexpr int NEPI = EPI != EPI_NONE ? 16 : 4;
+        constexpr int NSTEP = NEPI + 6;
+        float et[4];
+        uint32_t h01 = 0, h23 = 0, l01 = 0;
+        float r0 = 0.f, r1 = 0.f;
+        f32x4 ev;
+        auto fence = [](float &x) { asm volatile("" : "+v"(x)); };
+        auto epi_step = [&](int k, int p) {
+            if (k < NEPI) {
+                const int e = k & 3;
+                if constexpr (EPI == EPI_NONE) {
+                    float y = ev[e] * sc.inv;
+                    fence(y);
+                    ev[e] = y;
+                    return;
+                }
+                switch (k >> 2) {
+                case 0: et[e] = __builtin_amdgcn_exp2f(ev[e] * sc.c1); fence(et[e]); break;
+                case 1: et[e] = __builtin_fmaf(et[e], et[e] + 2.0f, 2.0f); fence(et[e]); break;
+                case 2: et[e] = __builtin_fmaf(sc.k2, __builtin_amdgcn_rcpf(et[e]), sc.inv); fence(et[e]); break;
+                default: { float y = ev[e] * et[e]; fence(y); ev[e] = y; } break;
+                }
+                return;
+            }
+            const int n = nt_of<l>(wave, jp(p)) * 16 + 4 * q;
+            char *o = lds + out_off(l) + (ct_of<l>(wave, cp(p)) * 16 + col) * L::out_rs(l) + n * 2;
+            switch (k - NEPI) {
+            case 0: h01 = pk_f16(ev.x, ev.y); h23 = pk_f16(ev.z, ev.w); break;
+            case 1: r0 = rem_f16<0>(h01, ev.x); r1 = rem_f16<1>(h01, ev.y); break;
+            case 2: l01 = pk_f16(r0, r1); *reinterpret_cast<u32x2 *>(o) = u32x2{h01, h23}; break;
+            case 3: r0 = rem_f16<0>(h23, ev.z); r1 = rem_f16<1>(h23, ev.w); break;
+            case 4: h23 = pk_f16(r0, r1); break;
+            default: *reinterpret_cast<u32x2 *>(o + L::out_pl(l)) = u32x2{l01, h23}; break;
+            }
+        };
+        u32x4 xb[3][2];
+        ldx(xb[0], 0);
+        if (NI > 1) ldx(xb[1], 1);
+        f32x4 acc = init_of(0), nxt = acc;
+        ev = acc;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            if (p + 1 < NP) nxt = init_of(p + 1);
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc) {
+                const int i = p * KC + kc;
+                if (i + 2 < NI) ldx(xb[(i + 2) % 3], i + 2);
+#pragma unroll
+                for (int m = 0; m < 3; ++m) {
+                    acc = mm1(jp(p), kc, m, xb[i % 3], acc);
+                    const int s = kc * 3 + m, g = p * NMF + s;
+                    if (p > 0)
+#pragma unroll
+                        for (int u = s * NSTEP / NMF; u < (s + 1) * NSTEP / NMF; ++u) epi_step(u, p - 1);
+#pragma unroll
+                    for (int k = (g * NS + TOT - 1) / TOT; k < ((g + 1) * NS + TOT - 1) / TOT; ++k) side(k);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            ev = acc;
+            acc = nxt;
+        }
+#pragma unroll
+        for (int u = 0; u < NSTEP; ++u) epi_step(u, NP - 1);
+    }
+
+    template <int l, int NS = 0, class SIDE>
+    static MPCD_DEV void layer_v(const WF<l> &w, SIDE side, const Sc sc, char *lds, int wave, int lane)
+    {
+        hidden<l, NS>([&](int j, int kc, int m, const u32x4 (&x)[2], f32x4 acc) { return mfma_h(w.v[j][kc][wpl(m)], x[xpl(m)], acc); },
+                      side, sc, lds, wave, lane);
+    }
+    template <int l, int NS = 0, class SIDE>
+    static MPCD_DEV void layer_a(const WF<l> &w, SIDE side, const Sc sc, char *lds, int wave, int lane)
+    {
+        hidden<l, NS>(
+            [&](int j, int kc, int m, const u32x4 (&x)[2], f32x4 acc) {
+                const bool first = kc == 0 && m == 0, last = kc == KCL<l> - 1 && m == 2;
+                if (first && last) return mfma_h_agpr<true, true>(w.v[j][kc][wpl(m)], x[xpl(m)], acc);
+                if (first) return mfma_h_agpr<true, false>(w.v[j][kc][wpl(m)], x[xpl(m)], acc);
+                if (last) return mfma_h_agpr<false, true>(w.v[j][kc][wpl(m)], x[xpl(m)], acc);
+                return mfma_h_agpr<false, false>(w.v[j][kc][wpl(m)], x[xpl(m)], acc);
+            },
+            side, sc, lds, wave, lane);
+    }
+
+    // x (4 features) -> fp32 row in XB and the two fp16 planes layer 0 reads
+    static MPCD_DEV void store_x(char *lds, int cl, int n, const f32x4 &x)
+    {
+        *reinterpret_cast<f32x4 *>(lds + L::XB + (cl * L::SX + n) * 4) = x;
+        u32x2 hi, lo;
+        split2(x, hi, lo);
+        char *o = lds + L::S1 + cl * L::RS + n * 2;
+        *reinterpret_cast<u32x2 *>(o) = hi;
+        *reinterpret_cast<u32x2 *>(o + L::PL) = lo;
+    }
+
+    // final Linear (32 -> D0) + the denoise update (reference op order, mlp_rw.hip final_and_update): wave w ->
+    // n-tiles w + 4j, both column tiles (a candidate's two CFG rows in one lane)
+    static MPCD_DEV void final_and_update(const WF<13> &f, const Sc sc, char *lds, const MlpSampleArgs &p,
+                                          const StepPlan &sp, int s, int64_t cand0, const f32x4 (&nz)[NZT],
+                                          uint32_t (&am)[2], int wave, int lane)
+    {
+        constexpr int T = NZT, NT = D0 / 16;
+        const int col = lane & 15, q = lane >> 4;
+        const float *bias = reinterpret_cast<const float *>(lds + L::BI + A::boff(13) * 4);
+        f32x4 acc[T][2];
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            const int nt = (NT % 4 == 0 || wave + 4 * j < NT) ? wave + 4 * j : 0;
+            acc[j][0] = acc[j][1] = *reinterpret_cast<const f32x4 *>(bias + nt * 16 + 4 * q);
+        }
+#pragma unroll
+        for (int c = 0; c < NCT; ++c) {
+            const char *b = lds + L::T1 + (c * 16 + col) * L::RS + 8 * q * 2;
+            u32x4 x[2];
+            x[0] = *reinterpret_cast<const u32x4 *>(b);
+            x[1] = *reinterpret_cast<const u32x4 *>(b + L::PL);
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+                if (NT % 4 == 0 || wave + 4 * j < NT)
+#pragma unroll
+                    for (int m = 0; m < 3; ++m) acc[j][c] = mfma_h(f.v[j][0][wpl(m)], x[xpl(m)], acc[j][c]);
+        }
+#pragma unroll
+        for (int j = 0; j < T; ++j)
+#pragma unroll
+            for (int c = 0; c < NCT; ++c) acc[j][c] = acc[j][c] * sc.inv;  // eps = acc / s (exact scaling)
+        if (R == 16) {
+            // column c holds candidate c & 7's context row (c < 8) or masked row (c >= 8): bring the masked
+            // row's eps next to the context row's (DPP row_ror:8 swaps the two halves of each 16-lane row)
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float e = acc[j][0][r];
+                    acc[j][1][r] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, e), 0x128, 0xF, 0xF, false));
+                }
+            if (col >= 8) return;
+        }
+        const bool last = s == p.n_steps - 1;
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            const int nt = wave + 4 * j;
+            if (NT % 4 != 0 && nt >= NT) continue;
+            const int n = nt * 16 + 4 * q;
+            const int cl = col;
+            const f32x4 ec = acc[j][0], eu = acc[j][1];
+            const int64_t gc = cand0 + cl;
+            if (SMODE == MODE_EPS) {
+                if (gc < p.batch) {
+                    *reinterpret_cast<f32x4 *>(p.x_out + (size_t)gc * D0 + n) = ec;
+                    *reinterpret_cast<f32x4 *>(p.chain + (size_t)gc * D0 + n) = eu;
+                }
+                continue;
+            }
+            const f32x4 x = *reinterpret_cast<const f32x4 *>(lds + L::XB + (cl * L::SX + n) * 4);
+            f32x4 xn;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float xv = x[r];
+                const float x0c = sp.a * xv - sp.b * ec[r];
+                const float x0u = sp.a * xv - sp.b * eu[r];
+                float x0 = p.wp1 * x0c - p.wf * x0u;
+                x0 = clamp1(x0);
+                const float mean = sp.c1 * x0 + sp.c2 * xv;
+                const float o = (sp.flags & PLAN_NOISE) ? mean + sp.std * nz[j][r] : mean;
+                xn[r] = o;
+                am[0] = max(am[0], max(abs_bits(xv), abs_bits(o)));
+            }
+            store_x(lds, cl, n, xn);
+            if (gc < p.batch) {
+                if (p.chain) *reinterpret_cast<f32x4 *>(p.chain + ((size_t)(s + 1) * p.batch + gc) * D0 + n) = xn;
+                if (last) *reinterpret_cast<f32x4 *>(p.x_out + (size_t)gc * D0 + n) = xn;
+            }
+        }
+    }
+
+    // noise of step s (slice s + 1) for this lane's quads (injected noise, MODE_DDPM_XN; or Philox when not staged)
+    static MPCD_DEV void fetch_noise(f32x4 (&nz)[NZT], const MlpSampleArgs &p, const StepPlan &sp, int s, int64_t cand0,
+                                     int wave, int lane)
+    {
+        constexpr int NT = D0 / 16;
+#pragma unroll
+        for (int j = 0; j < NZT; ++j) nz[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (!IS_DDPM || !(sp.flags & PLAN_NOISE)) return;
+        const int col = lane & 15, q = lane >> 4;
+#pragma unroll
+        for (int j = 0; j < NZT; ++j) {
+            const int nt = wave + 4 * j;
+            if (NT % 4 != 0 && nt >= NT) continue;
+            const int n = nt * 16 + 4 * q;
+            const int64_t gc = cand0 + col;
+            if (gc >= p.batch || (R == 16 && col >= 8)) continue;
+            if (SMODE == MODE_DDPM_XN)
+                nz[j] = *reinterpret_cast<const f32x4 *>(p.noise + ((size_t)(s + 1) * p.batch + gc) * D0 + n);
+            else
+                nz[j] = philox_normal4(p.seed, (uint64_t)(p.global_offset + gc), (uint32_t)(s + 1), (uint32_t)(n >> 2));
+        }
+    }
+
+    // The next step's Philox draw as NPH micro-steps (mlp_rw.hip ph_*: the exact operations of common.h
+    // philox4x32_10 / philox_normal4, every intermediate through a register fence; bit-identical to fetch_noise)
+    struct PhSt {
+        uint32_t c0, c1, c2, c3, k0, k1, h;
+        float u0, u1, u2, u3, ra, rb;
+        float z[4];
+    };
+    static constexpr int NPH = 40 + 12;
+    static constexpr bool STAGED_NOISE = SMODE == MODE_DDPM_CFG && NZT == 1;
+    static MPCD_DEV void ph_init(PhSt &st, const MlpSampleArgs &p, int slice, int64_t cand0, int wave, int lane)
+    {
+        const int col = lane & 15, q = lane >> 4;
+        const int n = min(wave, D0 / 16 - 1) * 16 + 4 * q;
+        const uint64_t cand = (uint64_t)(p.global_offset + cand0 + col);
+        st.c0 = (uint32_t)(n >> 2);
+        st.c1 = (uint32_t)cand;
+        st.c2 = (uint32_t)(cand >> 32);
+        st.c3 = (uint32_t)slice;
+        st.k0 = (uint32_t)p.seed;
+        st.k1 = (uint32_t)(p.seed >> 32);
+    }
+    static MPCD_DEV void ph_step(PhSt &st, int k)
+    {
+        auto fu = [](uint32_t &x) { asm volatile("" : "+v"(x)); };
+        auto ff = [](float &x) { asm volatile("" : "+v"(x)); };
+        constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+        if (k < 40) {
+            switch (k & 3) {
+            case 0: st.h = __umulhi(M0, st.c0); fu(st.h); break;
+            case 1: st.c0 = M0 * st.c0; fu(st.c0); break;
+            case 2: { const uint32_t hi1 = __umulhi(M1, st.c2); st.c3 = st.h ^ st.c3 ^ st.k1; st.h = hi1; fu(st.h); fu(st.c3); } break;
+            default: {
+                const uint32_t lo1 = M1 * st.c2;
+                const uint32_t n0 = st.h ^ st.c1 ^ st.k0, n2 = st.c3, n3 = st.c0;
+                st.c0 = n0; st.c1 = lo1; st.c2 = n2; st.c3 = n3;
+                st.k0 += W0; st.k1 += W1;
+                fu(st.c0); fu(st.c1); fu(st.c2); fu(st.c3);
+            } break;
+            }
+            return;
+        }
+        const float S = 2.3283064365386963e-10f;  // 2^-32
+        switch (k - 40) {
+        case 0: st.u0 = ((float)st.c0 + 1.0f) * S; st.u1 = (float)st.c1 * S; ff(st.u0); ff(st.u1); break;
+        case 1: st.u2 = ((float)st.c2 + 1.0f) * S; st.u3 = (float)st.c3 * S; ff(st.u2); ff(st.u3); break;
+        case 2: st.ra = -2.0f * __logf(st.u0); ff(st.ra); break;
+        case 3: st.rb = -2.0f * __logf(st.u2); ff(st.rb); break;
+        case 4: st.ra = __fsqrt_rn(st.ra); ff(st.ra); break;
+        case 5: st.rb = __fsqrt_rn(st.rb); ff(st.rb); break;
+        case 6: st.u1 = 6.2831853071795865f * st.u1; st.u3 = 6.2831853071795865f * st.u3; ff(st.u1); ff(st.u3); break;
+        case 7: st.z[0] = __cosf(st.u1); ff(st.z[0]); break;
+        case 8: st.z[1] = __sinf(st.u1); ff(st.z[1]); break;
+        case 9: st.z[2] = __cosf(st.u3); ff(st.z[2]); break;
+        case 10: st.z[3] = __sinf(st.u3); ff(st.z[3]); break;
+        default:
+            for (int e = 0; e < 4; ++e) {
+                st.z[e] = (e < 2 ? st.ra : st.rb) * st.z[e];
+                ff(st.z[e]);
+            }
+            break;
+        }
+    }
+    static MPCD_DEV void ph_take(f32x4 (&nz)[NZT], const PhSt &st, const StepPlan &sp, int64_t cand0,
+                                 const MlpSampleArgs &p, int wave, int lane)
+    {
+        const int col = lane & 15;
+        nz[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const bool ok = (sp.flags & PLAN_NOISE) && (D0 / 16 % 4 == 0 || wave < D0 / 16) && cand0 + col < p.batch &&
+                        !(R == 16 && col >= 8);
+        if (ok) nz[0] = f32x4{st.z[0], st.z[1], st.z[2], st.z[3]};
+    }
+
+    static MPCD_DEV void run(const MlpSampleArgs &p)
+    {
+        extern __shared__ float lds_f[];
+        char *lds = reinterpret_cast<char *>(lds_f);
+        const int lane = threadIdx.x & 63;
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const int64_t cand0 = (int64_t)blockIdx.x * CPW;
+        int lane16 = lane * 16;
+        const float *wp = p.wpack;
+        float *bi = reinterpret_cast<float *>(lds + L::BI);
+        float *bic = reinterpret_cast<float *>(lds + L::BIC);
+        float *cps = reinterpret_cast<float *>(lds + L::CPS);
+
+        // resident weights: Linear 2..7 in AGPRs (the asm MFMAs' "a" operands), 0, 1, 9..13 in VGPRs
+        WF<0> w0;
+        WF<1> w1;
+        WF<2> w2;
+        WF<3> w3;
+        WF<4> w4;
+        WF<5> w5;
+        WF<6> w6;
+        WF<7> w7;
+        WF<9> w9;
+        WF<10> w10;
+        WF<11> w11;
+        WF<12> w12;
+        WF<13> w13;
+        load_res<0>(w0, wp, wave, lane);
+        load_res<1>(w1, wp, wave, lane);
+        load_res<2>(w2, wp, wave, lane);
+        load_res<3>(w3, wp, wave, lane);
+        load_res<4>(w4, wp, wave, lane);
+        load_res<5>(w5, wp, wave, lane);
+        load_res<6>(w6, wp, wave, lane);
+        load_res<7>(w7, wp, wave, lane);
+        load_res<9>(w9, wp, wave, lane);
+        load_res<10>(w10, wp, wave, lane);
+        load_res<11>(w11, wp, wave, lane);
+        load_res<12>(w12, wp, wave, lane);
+        load_res<13>(w13, wp, wave, lane);
+        // biases x s_l (the accumulators run at each layer's weight scale); the cond tables are scaled per step
+        for (int l = 0; l < NLAYER; ++l) {
+            const float s = ldc(wp + l);
+            for (int i = threadIdx.x; i < A::N[l]; i += H2_T) bi[A::boff(l) + i] = wp[woffh<D0>(l) + A::K[l] * A::N[l] + i] * s;
+        }
+        for (int j = 0; j < 6; ++j)
+            for (int i = threadIdx.x; i < A::N[2 * j + 1]; i += H2_T)
+                bic[cond_off(j) + i] = wp[woffh<D0>(2 * j + 1) + A::K[2 * j + 1] * A::N[2 * j + 1] + i];
+        for (int i = threadIdx.x; i < COND_TOTAL; i += H2_T) cps[i] = CTX ? p.cproj[i] : 0.f;
+        if (threadIdx.x < CPW) reinterpret_cast<uint32_t *>(lds + L::AMX)[threadIdx.x] = 0u;
+        uint32_t am[2] = {0u, 0u};
+        for (int i = threadIdx.x; i < CPW * QUADS; i += H2_T) {  // x_T (fp32 + planes)
+            const int c = i / QUADS, qd = i - c * QUADS;
+            const int64_t gc = cand0 + c;
+            f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (gc < p.batch) {
+                z = p.noise ? *reinterpret_cast<const f32x4 *>(p.noise + (size_t)gc * D0 + qd * 4)
+                            : philox_normal4(p.seed, (uint64_t)(p.global_offset + gc), 0u, (uint32_t)qd);
+                if (p.chain && SMODE != MODE_EPS) *reinterpret_cast<f32x4 *>(p.chain + (size_t)gc * D0 + qd * 4) = z;
+            }
+            store_x(lds, c, qd * 4, z);
+        }
+
+        f32x4 nz[NZT];
+        StepPlan sp = load_plan(p.plan, 0);
+        fetch_noise(nz, p, sp, 0, cand0, wave, lane);
+        // this thread's f32x4 of the per-step cond tables: columns 4k..4k+3 of the 448 (one cond block) for the
+        // context rows (TPC, k < 112) or the masked rows (TPU); its layer's weight scale
+        const bool tp_thread = threadIdx.x < COND_TOTAL / 2;
+        const bool ctx_half = threadIdx.x >= COND_TOTAL / 4;
+        const int tpi = tp_thread ? (ctx_half ? (int)threadIdx.x - COND_TOTAL / 4 : (int)threadIdx.x) : 0;
+        const int tcol = tpi * 4;
+        const int tblk = tcol < 32 ? 0 : tcol < 96 ? 1 : tcol < 224 ? 2 : tcol < 352 ? 3 : tcol < 416 ? 4 : 5;
+        const float tscale = p.wpack[2 * tblk + 1];  // s of cond layer 2 * block + 1
+        f32x4 tpre = reinterpret_cast<const f32x4 *>(p.tproj)[tpi];
+        auto bar = [] { lds_barrier(); };
+        int wofs = 0;
+
+        bar();  // x_T, tables and biases staged
+        for (int s = 0; s < p.n_steps; ++s) {
+            // launder the pack base each step: the streamed layer's loads and the layers' scale constants (scalar
+            // loads, 42 SGPRs if hoisted) stay inside the loop
+            asm volatile("" : "+s"(wofs), "+v"(lane16));
+            const float *ws = wp + wofs;
+            auto none = [](int) {};
+            // this step's time projections + cond biases (+ shared context part), x the cond layer's weight scale
+            if (tp_thread) {
+                f32x4 u = tpre + reinterpret_cast<const f32x4 *>(lds + L::BIC)[tpi];
+                if (ctx_half) u = u + reinterpret_cast<const f32x4 *>(lds + L::CPS)[tpi];
+                reinterpret_cast<f32x4 *>(lds + (ctx_half ? L::TPC : L::TPU))[tpi] = u * tscale;
+            }
+            tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 1 < p.n_steps ? s + 1 : s) * COND_TOTAL)[tpi];
+            layer_v<0>(w0, none, sc_of(ws, 0), lds, wave, lane);
+            bar();
+            layer_v<1>(w1, none, sc_of(ws, 1), lds, wave, lane);
+            bar();
+            layer_a<2>(w2, none, sc_of(ws, 2), lds, wave, lane);
+            bar();
+            layer_a<3>(w3, none, sc_of(ws, 3), lds, wave, lane);
+            bar();
+            layer_a<4>(w4, none, sc_of(ws, 4), lds, wave, lane);
+            bar();
+            layer_a<5>(w5, none, sc_of(ws, 5), lds, wave, lane);
+            bar();
+            // the next step's Philox draw in Linear 6's MFMA slots (resident weights: the fewest live VGPRs)
+            PhSt ph;
+            if constexpr (STAGED_NOISE) {
+                ph_init(ph, p, s + 2, cand0, wave, lane);  // step s + 1's noise is Philox slice s + 2 (fetch_noise)
+                layer_a<6, NPH>(w6, [&](int k) { ph_step(ph, k); }, sc_of(ws, 6), lds, wave, lane);
+            } else {
+                layer_a<6>(w6, none, sc_of(ws, 6), lds, wave, lane);
+            }
+            bar();
+            WF<8> w8;
+            layer_a<7, NFRAG<8>>(w7, [&](int k) { load_st1<8>(w8, ws, wave, lane16, k); }, sc_of(ws, 7), lds, wave, lane);
+            bar();
+            const StepPlan cur = sp;
+            if (s + 1 < p.n_steps) sp = load_plan(p.plan, s + 1);
+            layer_v<8>(w8, none, sc_of(ws, 8), lds, wave, lane);
+            bar();
+            layer_v<9>(w9, none, sc_of(ws, 9), lds, wave, lane);
+            bar();
+            layer_v<10>(w10, none, sc_of(ws, 10), lds, wave, lane);
+            f32x4 nzc[NZT];
+#pragma unroll
+            for (int j = 0; j < NZT; ++j) nzc[j] = nz[j];
+            if (STAGED_NOISE && s + 1 < p.n_steps) ph_take(nz, ph, sp, cand0, p, wave, lane);
+            else if (s + 1 < p.n_steps) fetch_noise(nz, p, sp, s + 1, cand0, wave, lane);
+            bar();
+            layer_v<11>(w11, none, sc_of(ws, 11), lds, wave, lane);
+            bar();
+            layer_v<12>(w12, none, sc_of(ws, 12), lds, wave, lane);
+            bar();
+            final_and_update(w13, sc_of(ws, 13), lds, p, cur, s, cand0, nzc, am, wave, lane);
+            bar();  // x planes of the next step written; this step's last reads of TPC / TPU long done
+        }
+        if (SMODE != MODE_EPS && p.chain_absmax) {
+            const int col = lane & 15;
+            store_chain_absmax<CPW, H2_T>(reinterpret_cast<uint32_t *>(lds + L::AMX), am, col, -1, R == 32 || col < 8,
+                                          p.chain_absmax, cand0, p.batch);
+        }
+    }
+};
+
+template <int D0, int SMODE, bool CTX, int R>
+__global__ __launch_bounds__(H2_T, 1) void mlp_h2_kernel(const MlpSampleArgs p)
+{
+    MlpH2<D0, SMODE, CTX, R>::run(p);
+}
+
+template <int D0, int SMODE, bool CTX, int R>
+hipError_t launch_h2_r(const MlpSampleArgs &a, hipStream_t stream)
+{
+    using L = Lds2<D0, 2, R>;
+    static_assert(L::total <= 160 * 1024, "LDS budget (160 KiB per CU)");
+    if (hipError_t e = allow_max_lds<&mlp_h2_kernel<D0, SMODE, CTX, R>>(); e != hipSuccess) return e;
+    const int64_t blocks = (a.batch + L::CPW - 1) / L::CPW;
+    hipLaunchKernelGGL((mlp_h2_kernel<D0, SMODE, CTX, R>), dim3((unsigned)blocks), dim3(H2_T), (size_t)L::total, stream, a);
+    return hipGetLastError();
+}
+
+template <int D0, int SMODE, bool CTX>
+hipError_t launch_h2(const MlpSampleArgs &a, int rows, hipStream_t stream)
+{
+    return rows == 16 ? launch_h2_r<D0, SMODE, CTX, 16>(a, stream) : launch_h2_r<D0, SMODE, CTX, 32>(a, stream);
+}
+
+template <int D0>
+hipError_t launch_h2_d0(const MlpSampleArgs &a, int rows, hipStream_t stream)
+{
+    const bool ctx = a.cproj != nullptr;
+    switch (a.mode) {
+    case MODE_DDPM_CFG:
+        if (a.noise) return ctx ? launch_h2<D0, MODE_DDPM_XN, true>(a, rows, stream) : launch_h2<D0, MODE_DDPM_XN, false>(a, rows, stream);
+        return ctx ? launch_h2<D0, MODE_DDPM_CFG, true>(a, rows, stream) : launch_h2<D0, MODE_DDPM_CFG, false>(a, rows, stream);
+    case MODE_EPS: return ctx ? launch_h2<D0, MODE_EPS, true>(a, rows, stream) : launch_h2<D0, MODE_EPS, false>(a, rows, stream);
+    }
+    return hipErrorInvalidValue;
+}
+
+uint16_t f16_rne(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+
+}  // namespace
+
+bool mlp_h2_supports(int d0, int mode) { return (d0 == 32 || d0 == 64) && (mode == MODE_DDPM_CFG || mode == MODE_EPS); }
+
+int mlp_packed_floats_h2(int d0)
+{
+    switch (d0) {
+    case 32: return woffh<32>(NLAYER);
+    case 64: return woffh<64>(NLAYER);
+    default: return -1;
+    }
+}
+
+// Linear l (torch weight [N][K]) -> s_l = 2^(10 - ceil(log2 max |w|)), then w s_l = hi + lo (two fp16, round to
+// nearest even, lo the rounded remainder), packed as the MFMA A operand of v_mfma_f32_16x16x32_f16: chunk
+// (nt, kc, plane) = 64 lanes x 8 halves, lane l holding W[nt*16 + (l&15)][kc*32 + 8*(l>>4) + j], j = 0..7; then the
+// fp32 bias [N] (unscaled: the kernel scales it). Header: s, 1/s, fp32(log2 e)/s, -2/s per layer.
+void mlp_pack_weights_h2(int d0, const float *const *lin_w, const float *const *lin_b, float *out)
+{
+    const int Ks[NLAYER] = {d0, 32, 32, 64, 64, 128, 128, 128, 256, 64, 128, 32, 32, 32};
+    const int Ns[NLAYER] = {32, 32, 64, 64, 128, 128, 128, 128, 64, 64, 32, 32, 32, d0};
+    for (int i = 0; i < HDR; ++i) out[i] = 0.f;
+    size_t o = HDR;
+    for (int l = 0; l < NLAYER; ++l) {
+        const int K = Ks[l], N = Ns[l], KC = K / 32, NT = N / 16;
+        float mx = 0.f;
+        for (size_t i = 0; i < (size_t)K * N; ++i) mx = fmaxf(mx, fabsf(lin_w[l][i]));
+        int e = 0;
+        if (mx > 0.f && mx == mx) {
+            int ex;
+            frexpf(mx, &ex);  // mx in [2^(ex-1), 2^ex)
+            e = 10 - ex;
+            if (ldexpf(mx, e) > 1024.f) --e;
+        }
+        const float s = ldexpf(1.f, e), inv = ldexpf(1.f, -e);
+        out[l] = s;
+        out[16 + l] = inv;
+        out[32 + l] = 1.44269504088896341f * inv;
+        out[48 + l] = -2.f * inv;
+        uint16_t *pk = reinterpret_cast<uint16_t *>(out + o);
+        for (int nt = 0; nt < NT; ++nt)
+            for (int kc = 0; kc < KC; ++kc)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int j = 0; j < 8; ++j) {
+                        const float w = lin_w[l][(size_t)(nt * 16 + (lane & 15)) * K + kc * 32 + 8 * (lane >> 4) + j] * s;
+                        const uint16_t h = f16_rne(w);
+                        const uint16_t lo = f16_rne(w - (float)__builtin_bit_cast(_Float16, h));
+                        pk[(((size_t)(nt * KC + kc) * 2 + 0) * 64 + lane) * 8 + j] = h;
+                        pk[(((size_t)(nt * KC + kc) * 2 + 1) * 64 + lane) * 8 + j] = lo;
+                    }
+        o += (size_t)K * N;
+        for (int n = 0; n < N; ++n) out[o + n] = lin_b[l][n];
+        o += N;
+    }
+}
+
+// rows: 32 or 16 per workgroup (the same choice as the bf16x3 kernels: 16 below one 32-row workgroup per CU)
+hipError_t launch_mlp_h2(int d0, int rows, const MlpSampleArgs &a, hipStream_t stream)
+{
+    if (a.cproj && a.cproj_stride != 0) return hipErrorInvalidValue;  // shared context only
+    switch (d0) {
+    case 32: return launch_h2_d0<32>(a, rows, stream);
+    case 64: return launch_h2_d0<64>(a, rows, stream);
+    }
+    return hipErrorInvalidValue;
+}

@@ -224,7 +224,9 @@ int check_desc(const mpcd_net_desc *d)
     for (int i = 0; i < d->n_mults; ++i)
         if (d->mults[i] < 1) return fail(MPCD_EINVAL, "bad dim_mults");
     if (d->dtype == MPCD_F16 && d->kind != MPCD_NET_UNET) return fail(MPCD_EUNSUP, "MPCD_F16 is UNet-only");
-    if (d->dtype != MPCD_F32 && d->dtype != MPCD_F32X3 && d->dtype != MPCD_F16) return fail(MPCD_EINVAL, "bad dtype %d", d->dtype);
+    if (d->dtype == MPCD_F16X2 && d->kind != MPCD_NET_MLP) return fail(MPCD_EUNSUP, "MPCD_F16X2 is MLP-only");
+    if (d->dtype != MPCD_F32 && d->dtype != MPCD_F32X3 && d->dtype != MPCD_F16 && d->dtype != MPCD_F16X2)
+        return fail(MPCD_EINVAL, "bad dtype %d", d->dtype);
     return MPCD_OK;
 }
 
@@ -259,7 +261,8 @@ struct mpcd_ctx {
     int cond_dim = 0, cond_total = 0, n_cond = 0;
     DevBuf params;      // raw blob (time MLP, cond layers, UNet tensors)
     DevBuf wpack;       // MLP packed linear layers (fp32 MFMA operand order)
-    DevBuf wpack3;      // MLP linear layers split into three bf16 planes (MPCD_F32X3)
+    DevBuf wpack3;      // MLP linear layers split into three bf16 planes (MPCD_F32X3, and MPCD_F16X2's other cases)
+    DevBuf wpackh;      // MLP linear layers as two fp16 planes + per-layer scales (MPCD_F16X2)
     DevBuf cond_layers; // CondLayer[n_cond]
     UnetWeights unet{}; // device pointers into `params` + repacked conv weights
     DevBuf unet_pack;
@@ -435,11 +438,17 @@ int upload_net(mpcd_ctx *c, const mpcd_net_desc &d, const float *blob, size_t n_
         rc = c->wpack.ensure(packed.size() * sizeof(float));
         if (rc) return rc;
         HIP_TRY(hipMemcpy(c->wpack.p, packed.data(), packed.size() * sizeof(float), hipMemcpyHostToDevice));
-        if (d.dtype == MPCD_F32X3) {
+        if (d.dtype == MPCD_F32X3 || d.dtype == MPCD_F16X2) {
             std::vector<float> packed3((size_t)mlp_packed_floats_x3(d0));
             mlp_pack_weights_x3(d0, lw, lb, packed3.data());
             if ((rc = c->wpack3.ensure(packed3.size() * sizeof(float)))) return rc;
             HIP_TRY(hipMemcpy(c->wpack3.p, packed3.data(), packed3.size() * sizeof(float), hipMemcpyHostToDevice));
+        }
+        if (d.dtype == MPCD_F16X2 && mlp_packed_floats_h2(d0) > 0) {
+            std::vector<float> packedh((size_t)mlp_packed_floats_h2(d0));
+            mlp_pack_weights_h2(d0, lw, lb, packedh.data());
+            if ((rc = c->wpackh.ensure(packedh.size() * sizeof(float)))) return rc;
+            HIP_TRY(hipMemcpy(c->wpackh.p, packedh.data(), packedh.size() * sizeof(float), hipMemcpyHostToDevice));
         }
     } else {
         rc = unet_prepare(d, spec.size(), [&](const char *n) -> const float * {
@@ -465,12 +474,27 @@ int upload_net(mpcd_ctx *c, const mpcd_net_desc &d, const float *blob, size_t n_
 }  // namespace
 
 namespace {
-// MLP kernel choice: the split-bf16 kernel when the net asks for it and the context is shared (or
-// absent), else the exact-f32 kernel. Both are GPU kernels with fp32-level results.
+// MLP kernel choice (mlp_kernel_of): the two-term fp16 kernel for an MPCD_F16X2 net where it applies (CFG-DDPM or
+// the eps forward, H*d 32 / 64, shared context), the split-bf16 kernels for MPCD_F32X3 / the other MPCD_F16X2 cases
+// with a shared (or no) context, else the exact-f32 kernel. All are GPU kernels with fp32-level results.
+enum { MLPK_F32 = 0, MLPK_X3 = 1, MLPK_H2 = 2 };
+int mlp_kernel_of(const mpcd_ctx *c, int mode, bool shared_ctx)
+{
+    const int d0 = c->desc.horizon * c->desc.state_dim;
+    if (c->desc.dtype == MPCD_F16X2 && shared_ctx && c->wpackh.p && mlp_h2_supports(d0, mode)) return MLPK_H2;
+    if ((c->desc.dtype == MPCD_F32X3 || c->desc.dtype == MPCD_F16X2) && shared_ctx) return MLPK_X3;
+    return MLPK_F32;
+}
 hipError_t launch_mlp(mpcd_ctx *c, MlpSampleArgs &m, int nb, hipStream_t st)
 {
     const int d0 = c->desc.horizon * c->desc.state_dim;
-    if (c->desc.dtype == MPCD_F32X3 && (m.cproj == nullptr || m.cproj_stride == 0)) {
+    const int k = mlp_kernel_of(c, m.mode, m.cproj == nullptr || m.cproj_stride == 0);
+    if (k == MLPK_H2) {
+        m.wpack = c->wpackh.as<float>();
+        const int lay = mlp_x3_layout_of(m.batch, nb);  // the bf16x3 layouts' row choice: 16x8, 16x4, rw16 -> 16 rows
+        return launch_mlp_h2(d0, (lay == 1 || lay == 2 || lay == 4) ? 16 : 32, m, st);
+    }
+    if (k == MLPK_X3) {
         m.wpack = c->wpack3.as<float>();
         return launch_mlp_x3(d0, nb, m, st);
     }
@@ -541,7 +565,7 @@ void mpcd_destroy(mpcd_ctx *c)
 {
     if (!c) return;
     DeviceGuard device_guard_(c->device);
-    for (DevBuf *b : {&c->params, &c->wpack, &c->wpack3, &c->cond_layers, &c->unet_pack, &c->plan, &c->tproj, &c->cproj, &c->flag,
+    for (DevBuf *b : {&c->params, &c->wpack, &c->wpack3, &c->wpackh, &c->cond_layers, &c->unet_pack, &c->plan, &c->tproj, &c->cproj, &c->flag,
                       &c->unet_ws, &c->step_ctx, &c->step_part, &c->step_out, &c->step_amax})
         b->release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -812,6 +836,21 @@ int mpcd_unet_form(mpcd_ctx *c, int32_t sampler, int32_t out[4])
     if (sampler < MPCD_DDPM_CFG || sampler > MPCD_DDIM) return fail(MPCD_EINVAL, "bad sampler %d", sampler);
     if (!c->unet.ready) return fail(MPCD_ESTATE, "U-Net parameters not loaded");
     unet_form(c->unet, sampler, out);
+    return MPCD_OK;
+}
+
+int mpcd_mlp_form(mpcd_ctx *c, int32_t sampler, int64_t batch, int32_t out[3])
+{
+    if (!c || !out || batch < 1) return fail(MPCD_EINVAL, "bad argument");
+    if (!c->net_loaded || c->desc.kind != MPCD_NET_MLP) return fail(MPCD_EUNSUP, "not an MLP context");
+    if (sampler < MPCD_DDPM_CFG || sampler > MPCD_DDIM) return fail(MPCD_EINVAL, "bad sampler %d", sampler);
+    DEVICE_GUARD(c->device);
+    const int nb = c->desc.cfg_masked ? 2 : 1;
+    const int lay = mlp_x3_layout_of(batch, nb);
+    const int k = mlp_kernel_of(c, sampler, true);
+    out[0] = k;
+    out[1] = k == MLPK_X3 ? lay : -1;
+    out[2] = (lay == 1 || lay == 2 || lay == 4) ? 16 : 32;
     return MPCD_OK;
 }
 

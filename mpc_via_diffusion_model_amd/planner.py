@@ -80,7 +80,9 @@ class NetSpec:
     time_emb_dim: int = 32
     cfg: bool = True          # 4-arg net with the CFG context mask
     # GEMM numerics (include/mpcd.h mpcd_dtype): "f32" exact fp32 MFMA; "f32x3" fp32-accurate split-bf16
-    # MFMA (MLP: shared or no context; UNet: any); "f16" fp16 operands / fp32 accumulate (UNet, cfg 5)
+    # MFMA (MLP: shared or no context; UNet: any); "f16" fp16 operands / fp32 accumulate (UNet, cfg 5); "f16x2"
+    # fp32-class two-term fp16 MFMA (MLP: the CFG-DDPM sampler / eps forward at H*d 32 or 64 with a shared context;
+    # the other cases of such a net run its f32x3 kernels)
     dtype: str = "f32"
 
     def desc(self):
@@ -92,7 +94,7 @@ class NetSpec:
             d.mults[i] = m
         d.time_emb_dim = self.time_emb_dim
         d.cfg_masked = 1 if self.cfg else 0
-        dtypes = {"f32": N.MPCD_F32, "f16": N.MPCD_F16, "f32x3": N.MPCD_F32X3}
+        dtypes = {"f32": N.MPCD_F32, "f16": N.MPCD_F16, "f32x3": N.MPCD_F32X3, "f16x2": N.MPCD_F16X2}
         if self.dtype not in dtypes:
             raise ValueError(f"dtype {self.dtype!r}: use one of {sorted(dtypes)}")
         d.dtype = dtypes[self.dtype]
@@ -342,6 +344,14 @@ class DiffusionMPC:
         with torch.cuda.device(self.device):  # the library decides on the current device's CU count
             N.check(self._lib.mpcd_mlp_layout(int(n_samples), int(self.spec.cfg), ctypes.byref(out)), "mpcd_mlp_layout")
         return {v: k for k, v in MLP_LAYOUTS.items()}[out.value]
+
+    def mlp_form(self, n_samples, sample_fn="ddpm_cfg"):
+        """The MLP kernel a shared-context sample call of n_samples runs (mpcd_mlp_form): {"kernel": "f32" | "x3" |
+        "h2", "layout": the bf16x3 layout name or None, "rows_per_workgroup": 32 | 16}."""
+        out = (ctypes.c_int32 * 3)()
+        N.check(self._lib.mpcd_mlp_form(self._ctx, self._sampler_id(sample_fn), int(n_samples), out), "mpcd_mlp_form")
+        lay = {v: k for k, v in MLP_LAYOUTS.items()}.get(out[1]) if out[1] >= 0 else None
+        return {"kernel": ("f32", "x3", "h2")[out[0]], "layout": lay, "rows_per_workgroup": int(out[2])}
 
     def last_sample_ms(self):
         ms = ctypes.c_float()

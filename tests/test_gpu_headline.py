@@ -28,13 +28,17 @@ pytestmark = pytest.mark.gpu
 CASES = {"cfg1": (64, 16, 2, 4, 50), "cfg2": (4096, 32, 2, 4, 100)}
 
 
+@pytest.mark.parametrize("dtype", ["f32x3", "f16x2"])
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_timed_mpc_step_matches_oracle_full_batch(name):
+def test_timed_mpc_step_matches_oracle_full_batch(name, dtype):
+    """Both fp32-class numerics of the MLP: the split-bf16 kernels (f32x3) and the two-term fp16 kernel (f16x2,
+    csrc/mlp_h2.hip: mlp_h2_kernel<64, DDPM_CFG, ctx, 32> at cfg2, <32, DDPM_CFG, ctx, 16> at cfg1)."""
     B, H, d, C, N = CASES[name]
     torch.set_num_threads(min(16, torch.get_num_threads()))
     net = make_mlp(d, H, C, seed=0)
-    spec = NetSpec("mlp", state_dim=d, horizon=H, context_dim=C, dtype="f32x3")
+    spec = NetSpec("mlp", state_dim=d, horizon=H, context_dim=C, dtype=dtype)
     plan = DiffusionMPC(spec, net.state_dict(), variance_schedule="exponential", n_diffusion_steps=N)
+    assert plan.mlp_form(B)["kernel"] == ("h2" if dtype == "f16x2" else "x3")
     system = systems.get("double_int2d")
     x0 = np.random.default_rng(1).uniform(-1, 1, C)
     seed = 2
@@ -59,5 +63,5 @@ def test_timed_mpc_step_matches_oracle_full_batch(name):
     # the applied trajectory is the winner's unnormalised row
     ref_row = u[res.best_index].numpy()
     np.testing.assert_allclose(res.u_best, ref_row, rtol=0, atol=1e-4)
-    print(f"{name}: B={B} worst trajectory rel {tr:.3e}, worst element {el:.3e}, "
+    print(f"{name} {dtype}: B={B} worst trajectory rel {tr:.3e}, worst element {el:.3e}, "
           f"max cost rel {float(np.max(np.abs(got - cost) / np.abs(cost))):.3e}, argmin {res.best_index} (oracle {i})")

@@ -1,6 +1,7 @@
 """GPU parity: persistent MLP sampler (CFG-DDPM, CFG-DDIM, DDIM) against the oracle, via the C ABI.
-Every test runs both GEMM numerics: "f32" (exact fp32 MFMA) and "f32x3" (split-bf16 MFMA), at the
-same tolerances."""
+Every test runs the three GEMM numerics: "f32" (exact fp32 MFMA), "f32x3" (split-bf16 MFMA) and "f16x2" (two-term
+fp16 MFMA where it applies: CFG-DDPM / eps at H*d 32 / 64 with a shared context; its other cases run the f32x3
+kernels), at the same tolerances."""
 import numpy as np
 import pytest
 import torch
@@ -14,7 +15,7 @@ from ._util import assert_traj_close, make_mlp, oracle_sensitivity
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["f32", "f32x3"])
+@pytest.fixture(params=["f32", "f32x3", "f16x2"])
 def dtype(request):
     return request.param
 

@@ -12,6 +12,8 @@
 #                       WRITE_SIZE + MFMA busy), tune cache shared       -> gpurun_out/uroof/<cfg>_*
 #   unet[:<cfg>]        tools/unet_perf.py timing of one sample call      -> gpurun_out/unet_<cfg>.log
 #   mlpab:<variant>     cfg2 bench with libmpcd_<variant>.so (experiment build) -> gpurun_out/mlpab_<variant>.log
+#   sqpmc[:<B>]        SQ instruction / wait / MFMA-busy counters of the cfg2 bench at B candidates (two passes)
+#                                                                         -> gpurun_out/prof/sqpmc_<B>_*
 #   l2pmc[:<workload>]  L1->L2 read requests and L2 hit / miss counters of that bench -> gpurun_out/prof/l2pmc_*
 #
 # Extra bench.py arguments for bench / trace / pmc come from $BENCH_ARGS; extra pytest arguments from
@@ -65,6 +67,15 @@ run_job() {
         timeout -s KILL 120 rocprofv3 --pmc $c -d "gpurun_out/prof/l2pmc_${w}_$i" -o run -f csv -- \
           python3 bench.py --workload "$w" --no-cpu-baseline --no-shard-probe --steps 3 --warmup 1 $BENCH_ARGS \
           > "gpurun_out/prof/l2pmc_${w}_$i.log" 2>&1 || return $?
+        i=$((i + 1))
+      done ;;
+    sqpmc)
+      local b=${arg:-4096} c i=0
+      for c in "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAVES" \
+               "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
+        timeout -s KILL 120 rocprofv3 --pmc $c -d "gpurun_out/prof/sqpmc_${b}_$i" -o run -f csv -- \
+          python3 bench.py --workload cfg2 --candidates "$b" --no-cpu-baseline --no-shard-probe --steps 3 --warmup 1 $BENCH_ARGS \
+          > "gpurun_out/prof/sqpmc_${b}_$i.log" 2>&1 || return $?
         i=$((i + 1))
       done ;;
     unet)
