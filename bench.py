@@ -2,7 +2,8 @@
 
 BASELINE.json metric "candidate trajectories/sec (100 denoise steps, H=32)". The default workload is
 configs[1] (cfg2): 2D double integrator, 4096 candidates per GPU, H=32, 100 CFG-DDPM steps, MLP
-noise-net (build-defined CFG MLP), fp32-accurate GEMMs. One step = one mpc_step,
+noise-net (build-defined CFG MLP), fp32-class GEMMs (two-term fp16, csrc/mlp_h2.hip; --dtype f32x3 for
+the six-product split-bf16 kernels). One step = one mpc_step,
 i.e. one mpcd_mpc_step call: context upload, Philox x_T + the denoising loop (2 net evaluations per
 step) + clip flag + fp64 rollout/cost + argmin + winner row (+ RCCL cost all-gather and winner
 exchange for N > 1) + one D2H copy of the applied trajectory. Weak scaling: every rank adds its
@@ -39,10 +40,10 @@ sys.path.insert(0, ROOT)
 WORKLOADS = {
     "cfg1": dict(workload="cfg1: 2D double integrator, MLP noise-net, CFG-DDPM (reference CPU-sized case)",
                  system="double_int2d", net="mlp", d=2, H=16, C=4, N=50, B=64, split=False, sampler="ddpm_cfg",
-                 ddim_steps=None, schedule="exponential", dtype="f32x3", mac=117504, mac_row=93184),
+                 ddim_steps=None, schedule="exponential", dtype="f16x2", mac=117504, mac_row=93184),
     "cfg2": dict(workload="cfg2: 2D double integrator, MLP noise-net, CFG-DDPM", system="double_int2d", net="mlp",
                  d=2, H=32, C=4, N=100, B=4096, split=False, sampler="ddpm_cfg", ddim_steps=None,
-                 schedule="exponential", dtype="f32x3", mac=119552, mac_row=95232),
+                 schedule="exponential", dtype="f16x2", mac=119552, mac_row=95232),
     "cfg3": dict(workload="cfg3: pendulum swing-up, 1D temporal U-Net, CFG-DDIM (100 sampling steps)",
                  system="pendulum", net="unet", d=1, H=32, C=2, N=100, B=16384, split=False, sampler="ddim_cfg",
                  ddim_steps=100, schedule="exponential", dtype="f32x3", mac=9122560 + 896 * (2 - 5), mac_row=None),
