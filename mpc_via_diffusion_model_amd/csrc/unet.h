@@ -141,6 +141,8 @@ struct UnetFusedStep {
 };
 UnetFusedPlan *unet_fused_prepare(const mpcd_net_desc &d, const UnetWeights &W, int rows_per_wg, std::string *why);
 size_t unet_fused_scratch_bytes(const UnetFusedPlan &pl, int64_t batch);
+// true: the fused launch writes each branch's eps (one row per workgroup) and the CFG update runs as its own launch
+bool unet_fused_split_update(const UnetFusedPlan &pl);
 int unet_fused_rows_per_wg(const UnetFusedPlan &pl);
 int unet_fused_n_ops(const UnetFusedPlan &pl);
 int unet_fused_prof_wgs();

@@ -839,7 +839,9 @@ size_t unet_workspace_bytes(const mpcd_net_desc &d, const UnetWeights &W, bool f
     const Dims m = dims_of(d);
     // + the sampler state x [B][H][d] and the per-quad chain |x| maxima [B][H*d/4]
     const size_t state = sizeof(float) * ((size_t)batch * m.H * m.d + (size_t)batch * (m.H * m.d / 4 + 1));
-    if (fused) return state + 256 + unet_fused_scratch_bytes(*W.fused, batch);
+    if (fused)  // + the eps of both branches when the update is its own launch (unet_fused_split_update)
+        return state + 256 + unet_fused_scratch_bytes(*W.fused, batch) +
+               (unet_fused_split_update(*W.fused) ? sizeof(float) * 2 * (size_t)batch * m.H * m.d + 256 : 0);
     return sizeof(float) * ws_floats(m, batch * nb) + state;
 }
 
@@ -869,6 +871,9 @@ int sample_fused(const mpcd_net_desc &d, const UnetWeights &W, const UnetSampleA
     f.x_out = a.x_out;
     f.amq = amq;
     f.scratch = scratch;
+    const bool split = unet_fused_split_update(pl);
+    float *eps_buf = split ? reinterpret_cast<float *>(scratch + (unet_fused_scratch_bytes(pl, a.batch) + 255) / 256 * 256)
+                           : nullptr;
     if (a.mode == MODE_EPS) {
         f.x = const_cast<float *>(a.x_in);  // read only in MODE_EPS
         f.tp = a.tproj;
@@ -894,8 +899,16 @@ int sample_fused(const mpcd_net_desc &d, const UnetWeights &W, const UnetSampleA
         f.step = s;
         f.last = s == a.n_steps - 1 ? 1 : 0;
         f.prof = s == 2 ? prof : nullptr;
+        if (split) {
+            f.eps_c = eps_buf;
+            f.eps_u = eps_buf + (size_t)a.batch * flat;
+        }
         hipError_t e = unet_fused_step(pl, f, st);
         if (e != hipSuccess) return uerr(MPCD_EHIP, std::string("fused U-Net: ") + hipGetErrorString(e));
+        if (split)
+            hipLaunchKernelGGL(update_kernel, dim3(g1), dim3(threads), 0, st, xs, eps_buf, a.batch, flat, a.plan, s, a.mode,
+                               a.clamp_x0, a.wp1, a.wf, a.noise, a.seed, a.global_offset, a.chain, a.x_out,
+                               s == a.n_steps - 1 ? 1 : 0, amq);
     }
     if (prof) {
         std::vector<uint64_t> h(prof_n);

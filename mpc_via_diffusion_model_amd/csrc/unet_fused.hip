@@ -44,6 +44,7 @@ using namespace mx;
 constexpr int kNtwMax = 2;   // n-tiles per wave a conv may get: 1 preferred (2 everywhere measured slower, DESIGN.md
                              // §4), 2 where a 4-wave workgroup has more n-tiles than waves
 constexpr int kGroups = 8;  // GroupNorm groups of every 32 / 64 / 128-channel conv (group_norm_n_groups)
+constexpr int kWprMax = 8;  // waves a row of one conv's output may span (GroupNorm partials cross them through LDS)
 
 enum { FK_SAME5 = 0, FK_DOWN3 = 1, FK_UP4 = 2, FK_PW1 = 3, FK_RESTORE = 4 };
 enum { FE_BIAS = 0, FE_GN = 1, FE_GN_COND = 2, FE_GN_RES = 3, FE_EPS = 4 };
@@ -118,7 +119,7 @@ constexpr Prog make_prog()
     pg.plb = offZ + regZ;
     pg.e_off = offZ;
     pg.stat_off = P * pg.plb;
-    pg.lds = pg.stat_off + 2 * 4 * R * kGroups * 2;  // cross-wave GroupNorm partials [S1 | S2][row][group][2]
+    pg.lds = pg.stat_off + 2 * 4 * R * kGroups * kWprMax;  // cross-wave GroupNorm partials [S1 | S2][row][group][part]
     auto view = [](int region, int L, int C, int ctot, int ch0) {
         CView v{};
         v.cs = cs_of(ctot ? ctot : C);
@@ -160,7 +161,7 @@ constexpr Prog make_prog()
             const int ncw = wc && ct % wc == 0 ? ct / wc : 0;
             if (ncw < 1 || (ncw << w) > 4 || (kind == FK_UP4 && (R * lin / 16) % ncw)) continue;
             const int wpr = gn && o.lout > 16 && (ncw * 16) % o.lout ? o.lout / (ncw * 16) : 1;
-            if (wpr > 2 || (wpr == 2 && o.lout != 2 * ncw * 16)) continue;
+            if (wpr > kWprMax || (wpr > 1 && (o.lout != wpr * ncw * 16 || (wpr & (wpr - 1))))) continue;
             o.ntw_sh = w;
             o.ncw = ncw;
             o.wpr = wpr;
@@ -478,7 +479,7 @@ MPCD_DEV void zero_halo()
 
 // ---- one conv of the program: GEMM + statistics + epilogue
 template <int P, int R, int H, int W, int I>
-MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
+MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, int brn, APre<P> &pre)
 {
     extern __shared__ __attribute__((aligned(16))) char sm[];
     using G = OpGeo<P, R, H, W, I>;
@@ -629,20 +630,28 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
     // squares); fixed order: the same bits for any batch, workgroup or tiling of the other ops.
     float mean[NTW][NCW], rstd[NTW][NCW];
     constexpr int QMASK = GN ? (1 << (op.cpg_sh - 2)) - 1 : 0;  // lane quarters per group - 1: 0, 1 or 3
-    if constexpr (GN && op.wpr == 2) {
-        // a row spans two waves (the wave's NCW tiles are one half of it): per-wave partial sums through LDS,
-        // added in wave order; two barriers per op
+    if constexpr (GN && op.wpr >= 2) {
+        // a row spans WPR waves (the wave's NCW tiles are one part of it): per-wave partial sums through LDS, added in
+        // wave order (the same order for every batch and workgroup); two barriers per op
+        constexpr int WPR = op.wpr;
         constexpr float inv_n = 1.0f / (float)(op.lout << op.cpg_sh);
-        float *st = reinterpret_cast<float *>(sm + ProgOf<P, R, H, W>::v.stat_off);  // [S1 | S2][row][group][half]
-        const int row = cr[0], half = (t0 / NCW) & 1;
+        float *st = reinterpret_cast<float *>(sm + ProgOf<P, R, H, W>::v.stat_off);  // [S1 | S2][row][group][part]
+        constexpr int S2 = R * kGroups * kWprMax;
+        const int row = cr[0], part = (t0 / NCW) & (WPR - 1);
         const bool leader = col == 0 && (q & QMASK) == 0;
+        auto sum_parts = [&](const float *p) {
+            float v = p[0];
+#pragma unroll
+            for (int i = 1; i < WPR; ++i) v = v + p[i];
+            return v;
+        };
         int slot[NTW];
         float m[NTW];
 #if MPCD_FUSED_GN1
-        // one pass, one barrier: both partial sums of each half row through LDS together
+        // one pass, one barrier: both partial sums of each part of the row through LDS together
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
-            slot[j] = (row * kGroups + (n0[j] >> op.cpg_sh)) * 2;
+            slot[j] = (row * kGroups + (n0[j] >> op.cpg_sh)) * kWprMax;
             f32x2 p1 = lo2(acc[j][0]) + hi2(acc[j][0]);
             f32x2 p2 = fma2(hi2(acc[j][0]), hi2(acc[j][0]), lo2(acc[j][0]) * lo2(acc[j][0]));
 #pragma unroll
@@ -654,17 +663,15 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
             float ss[2] = {p1[0] + p1[1], p2[0] + p2[1]};
             group_sum_n<16, QMASK, 2>(ss);
             if (leader) {
-                st[slot[j] + half] = ss[0];
-                st[2 * R * kGroups + slot[j] + half] = ss[1];
+                st[slot[j] + part] = ss[0];
+                st[S2 + slot[j] + part] = ss[1];
             }
         }
         lds_barrier();
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
-            const f32x2 w1 = *reinterpret_cast<const f32x2 *>(st + slot[j]);
-            const f32x2 w2 = *reinterpret_cast<const f32x2 *>(st + 2 * R * kGroups + slot[j]);
-            m[j] = (w1.x + w1.y) * inv_n;
-            const float rs = rsqrt_nr(fmaxf((w2.x + w2.y) * inv_n - m[j] * m[j], 0.f) + 1e-5f);
+            m[j] = sum_parts(st + slot[j]) * inv_n;
+            const float rs = rsqrt_nr(fmaxf(sum_parts(st + S2 + slot[j]) * inv_n - m[j] * m[j], 0.f) + 1e-5f);
 #pragma unroll
             for (int cc = 0; cc < NCW; ++cc) {
                 mean[j][cc] = m[j];
@@ -674,18 +681,17 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
 #else
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
-            slot[j] = (row * kGroups + (n0[j] >> op.cpg_sh)) * 2;
+            slot[j] = (row * kGroups + (n0[j] >> op.cpg_sh)) * kWprMax;
             f32x2 p1 = lo2(acc[j][0]) + hi2(acc[j][0]);
 #pragma unroll
             for (int cc = 1; cc < NCW; ++cc) p1 += lo2(acc[j][cc]) + hi2(acc[j][cc]);
             const float s1 = group_sum<16, QMASK>(p1[0] + p1[1]);
-            if (leader) st[slot[j] + half] = s1;
+            if (leader) st[slot[j] + part] = s1;
         }
         lds_barrier();
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
-            const f32x2 w1 = *reinterpret_cast<const f32x2 *>(st + slot[j]);
-            m[j] = (w1.x + w1.y) * inv_n;
+            m[j] = sum_parts(st + slot[j]) * inv_n;
             const f32x2 mm = {-m[j], -m[j]};
             f32x2 p2 = {0.f, 0.f};
 #pragma unroll
@@ -694,13 +700,12 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
                 p2 = fma2(d1, d1, fma2(d0, d0, p2));
             }
             const float s2 = group_sum<16, QMASK>(p2[0] + p2[1]);
-            if (leader) st[2 * R * kGroups + slot[j] + half] = s2;
+            if (leader) st[S2 + slot[j] + part] = s2;
         }
         lds_barrier();
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
-            const f32x2 w2 = *reinterpret_cast<const f32x2 *>(st + 2 * R * kGroups + slot[j]);
-            const float rs = rsqrt_nr((w2.x + w2.y) * inv_n + 1e-5f);
+            const float rs = rsqrt_nr(sum_parts(st + S2 + slot[j]) * inv_n + 1e-5f);
 #pragma unroll
             for (int cc = 0; cc < NCW; ++cc) {
                 mean[j][cc] = m[j];
@@ -820,10 +825,11 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
                 v[j][cc] = f32x4{y0[0], y0[1], y1[0], y1[1]};
             }
             if constexpr (EPI == FE_GN_COND) {
-                const bool masked = cr[cc] >= R / 2;
+                // R = 1: the workgroup's one row is branch brn of candidate cand0; else rows [0, R/2) context
+                const bool masked = R == 1 ? brn != 0 : cr[cc] >= R / 2;
                 f32x4 cv = masked || !shared_cp ? cv1[j] : cv1[j] + cvs[j];
                 if (!masked && a.cp && a.cp_stride) {
-                    const int64_t cand = cand0 + cr[cc];
+                    const int64_t cand = R == 1 ? cand0 : cand0 + cr[cc];
                     if (cand < a.batch) cv = cv + ldg4(a.cp + (size_t)cand * a.cp_stride + pp.cond_off + n0[j]);
                 }
                 v[j][cc] = v[j][cc] + cv;
@@ -905,7 +911,7 @@ MPCD_DEV void restore_op(const FArgs &a, int64_t row0)
 }
 
 template <int P, int R, int H, int W, int I>
-MPCD_DEV void run_ops(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
+MPCD_DEV void run_ops(const FArgs &a, int64_t cand0, int64_t row0, int brn, APre<P> &pre)
 {
     constexpr int N_OPS = ProgOf<P, R, H, W>::v.n;
     if constexpr (I < N_OPS) {
@@ -915,11 +921,11 @@ MPCD_DEV void run_ops(const FArgs &a, int64_t cand0, int64_t row0, APre<P> &pre)
             if constexpr (I + 1 < N_OPS) prefetch_op<P, R, H, W, I + 1>(a, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
                                                                      threadIdx.x & 63, pre);
         } else {
-            conv_op<P, R, H, W, I>(a, cand0, row0, pre);
+            conv_op<P, R, H, W, I>(a, cand0, row0, brn, pre);
         }
         lds_barrier();
         prof_mark(a, N_OPS, I, 3);
-        run_ops<P, R, H, W, I + 1>(a, cand0, row0, pre);
+        run_ops<P, R, H, W, I + 1>(a, cand0, row0, brn, pre);
     }
 }
 
@@ -938,7 +944,11 @@ __global__ __launch_bounds__(64 * W) void unet_fused_kernel(const FArgs a)
     // grid (MPCD_FUSED_PERSIST) keeps each CU's workgroups walking the net together, block after block, so the
     // weights of the ops in flight stay in the XCD's L2 instead of every late-starting workgroup re-fetching them.
     for (int64_t blk = blockIdx.x; blk < a.nblk; blk += gridDim.x) {
-    const int64_t cand0 = blk * RC, row0 = blk * R;
+    // R = 1 (the fp32-accurate H = 128 net, whose three-plane activations fit the LDS only one row at a time):
+    // workgroup blk runs branch blk & 1 of candidate blk >> 1 and writes that branch's eps; the CFG update of the
+    // two branches runs as its own launch (unet.hip update_kernel)
+    const int brn = R == 1 ? (int)(blk & 1) : 0;
+    const int64_t cand0 = R == 1 ? blk >> 1 : blk * RC, row0 = blk * R;
     // the first conv's weights are in flight while x is staged
     prefetch_op<P, R, H, W, 0>(a, __builtin_amdgcn_readfirstlane(tid >> 6), tid & 63, pre);
 
@@ -961,11 +971,20 @@ __global__ __launch_bounds__(64 * W) void unet_fused_kernel(const FArgs a)
     }
     lds_barrier();
 
-    run_ops<P, R, H, W, 0>(a, cand0, row0, pre);
+    run_ops<P, R, H, W, 0>(a, cand0, row0, brn, pre);
 
     // ---- the denoise update of this step (or the raw eps of both branches, MODE_EPS)
     const float *E = reinterpret_cast<const float *>(sm + pg.e_off);
     const int flat = H * d, quads = flat / 4;
+    if constexpr (R == 1) {  // this row's eps -> eps_c (context branch) / eps_u (masked branch); every mode
+        float *out = brn ? a.eps_u : a.eps_c;
+        if (cand0 < a.batch)
+            for (int i = tid; i < quads; i += FT)
+                *reinterpret_cast<f32x4 *>(out + (size_t)cand0 * flat + 4 * i) = *reinterpret_cast<const f32x4 *>(E + 4 * i);
+        if constexpr (!PERS) break;
+        lds_barrier();
+        continue;
+    }
     const StepPlan sp = a.plan ? a.plan[a.s] : StepPlan{};
     for (int i = tid; i < RC * quads; i += FT) {
         const int c = i / quads, qd = i - c * quads;
@@ -1008,8 +1027,9 @@ struct Cfg {
 // (1, 2, 64, 4): two or three 4-wave workgroups per CU, their barriers independent (cfg5 14.7 ms per CFG evaluation
 // vs 15.3 for one 8-wave workgroup of 4 rows); the split-bf16 nets keep 4-row blocks (their weights, three planes,
 // miss the L2 per block: cfg3 3.98 ms with 2-row blocks vs 3.58)
-#define MPCD_FUSED_CFGS C_(1, 2, 64, 4) C_(3, 4, 32, 8) C_(1, 8, 32, 8) C_(3, 2, 64, 8) C_(1, 2, 128, 8) C_(1, 4, 64, 8) \
-    C_(1, 2, 64, 8) C_(3, 2, 32, 4)
+// (3, 1, 128, 8): the fp32-accurate Panda net (H = 128), one row per workgroup, the CFG update as its own launch
+#define MPCD_FUSED_CFGS C_(1, 2, 64, 4) C_(3, 4, 32, 8) C_(1, 8, 32, 8) C_(3, 2, 64, 8) C_(1, 2, 128, 8) C_(3, 1, 128, 8) \
+    C_(1, 4, 64, 8) C_(1, 2, 64, 8) C_(3, 2, 32, 4)
 constexpr Cfg kCfgs[] = {
 #define C_(p, r, h, w) {p, r, h, w},
     MPCD_FUSED_CFGS
@@ -1138,11 +1158,15 @@ UnetFusedPlan *unet_fused_prepare(const mpcd_net_desc &d, const UnetWeights &W, 
     return pl;
 }
 
+// workgroups (row blocks) of one step: R / 2 candidates each, or (R = 1) one branch of one candidate each
+static int64_t fused_blocks(const UnetFusedPlan &pl, int64_t batch) { return pl.R == 1 ? 2 * batch : (batch + pl.R / 2 - 1) / (pl.R / 2); }
+
 size_t unet_fused_scratch_bytes(const UnetFusedPlan &pl, int64_t batch)
 {
-    const int64_t wgs = (batch + pl.R / 2 - 1) / (pl.R / 2);
-    return (size_t)wgs * pl.R * pl.prog->skip_elems_per_row * (pl.P == 1 ? 2 : 4);
+    return (size_t)fused_blocks(pl, batch) * pl.R * pl.prog->skip_elems_per_row * (pl.P == 1 ? 2 : 4);
 }
+
+bool unet_fused_split_update(const UnetFusedPlan &pl) { return pl.R == 1; }
 
 int unet_fused_rows_per_wg(const UnetFusedPlan &pl) { return pl.R; }
 int unet_fused_waves_per_wg(const UnetFusedPlan &pl) { return pl.W; }
@@ -1182,7 +1206,7 @@ hipError_t unet_fused_step(const UnetFusedPlan &pl, const UnetFusedStep &s, hipS
     fa.eps_u = s.eps_u;
     fa.scratch = static_cast<char *>(s.scratch);
     fa.prof = s.prof;
-    const int64_t grid = (s.batch + pl.R / 2 - 1) / (pl.R / 2);
+    const int64_t grid = fused_blocks(pl, s.batch);
     if (grid <= 0 || grid > 0x7fffffff) return hipErrorInvalidValue;
     fa.nblk = grid;
     return launch_any(pl.P, pl.R, pl.H, pl.W, fa, (unsigned)grid, st);

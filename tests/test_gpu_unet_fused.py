@@ -36,14 +36,19 @@ def _eps_err(got, ref):
     return float((got.cpu() - ref).abs().max()) / max(float(ref.abs().max()), 1.0)
 
 
-def test_fused_h128_f16_panda_shape(fused):
-    """H = 128 (the Panda net's horizon: d = 7, C = 20) has a fused program with fp16 operands only (the three
-    split-bf16 planes of its activations do not fit one CU's LDS): against the oracle and the layered path, and the
-    f32x3 planner at this horizon refuses the forced fused form."""
+@pytest.mark.parametrize("dtype", ["f16", "f32x3"])
+def test_fused_h128_panda_shape(dtype, fused):
+    """H = 128 (the Panda net's horizon: d = 7, C = 20): fp16 operands with two rows (both CFG branches) per workgroup,
+    and the fp32-accurate three-plane form with ONE row per workgroup (its activations fit one CU's LDS only one row
+    at a time: unet_fused_kernel<3, 1, 128, 8> writes each branch's eps and the CFG update runs as its own launch).
+    Forward against the oracle and the layered path, a CFG-DDPM chain (noise-free tail) against the oracle at the
+    dtype's bar, and Philox shard invariance."""
     d, H, C, B = 7, 128, 20, 3
     net = make_unet(d, C, seed=128)
-    plan = _planner(net, d, H, C, N=25, dtype="f16")
-    assert plan.unet_form()["fused"]
+    plan = _planner(net, d, H, C, N=25, dtype=dtype)
+    form = plan.unet_form()
+    assert form["fused"] and form["rows_per_workgroup"] == (1 if dtype == "f32x3" else 2)
+    tol = EPS_TOL[dtype]
     g = torch.Generator().manual_seed(7)
     x = torch.randn(B, H, d, generator=g)
     ctx = torch.rand(1, C, generator=g) * 2 - 1
@@ -54,15 +59,21 @@ def test_fused_h128_f16_panda_shape(fused):
             rc = net(x, tt, ctx.expand(B, C), torch.zeros(B, 1))
             ru = net(x, tt, ctx.expand(B, C), torch.ones(B, 1))
         e1, e2 = _eps_err(ec, rc), _eps_err(eu, ru)
-        assert max(e1, e2) <= EPS_TOL["f16"], f"f16 H=128 t={t}: {e1:.2e} {e2:.2e}"
+        assert max(e1, e2) <= tol, f"{dtype} H=128 t={t}: {e1:.2e} {e2:.2e}"
         force_unet_path("layered")
         lc, lu = plan.eps(x, t, ctx)
         force_unet_path("fused")
-        assert _eps_err(ec, lc.cpu()) <= EPS_TOL["f16"] and _eps_err(eu, lu.cpu()) <= EPS_TOL["f16"]
+        assert _eps_err(ec, lc.cpu()) <= tol and _eps_err(eu, lu.cpu()) <= tol
     full = plan.sample_trajectories(ctx, 5, H, seed=3, n_wo_noise=5)
     assert torch.equal(full[2:4], plan.sample_trajectories(ctx, 2, H, seed=3, n_wo_noise=5, global_offset=2))
-    with pytest.raises(Exception):
-        _planner(net, d, H, C, N=25, dtype="f32x3").eps(x, 3, ctx)
+    if dtype == "f32x3":
+        Bc, N = 4, 25
+        noise = torch.randn(N + 5 + 1, Bc, H, d, generator=torch.Generator().manual_seed(9))
+        ref = osam.ddpm_cfg(net, osch.buffers("exponential", N), ctx.expand(Bc, C), 0.01, Bc, H, n_wo_noise=5,
+                            noise=noise, return_chain=True)
+        got = plan.run_CFG(ctx, None, 0.01, n_samples=Bc, horizon=H, return_chain=True, noise=noise,
+                           n_diffusion_steps_without_noise=5)
+        assert_traj_close(got, ref, what="fused f32x3 H=128 chain")
 
 
 @pytest.mark.parametrize("dtype", ["f32x3", "f16"])

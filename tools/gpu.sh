@@ -70,11 +70,11 @@ run_job() {
         i=$((i + 1))
       done ;;
     sqpmc)
-      local b=${arg:-4096} c i=0
+      local b=${arg:-4096}${SQTAG} c i=0
       for c in "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAVES" \
                "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
         timeout -s KILL 120 rocprofv3 --pmc $c -d "gpurun_out/prof/sqpmc_${b}_$i" -o run -f csv -- \
-          python3 bench.py --workload cfg2 --candidates "$b" --no-cpu-baseline --no-shard-probe --steps 3 --warmup 1 $BENCH_ARGS \
+          python3 bench.py --workload cfg2 --candidates "${arg:-4096}" --no-cpu-baseline --no-shard-probe --steps 3 --warmup 1 $BENCH_ARGS \
           > "gpurun_out/prof/sqpmc_${b}_$i.log" 2>&1 || return $?
         i=$((i + 1))
       done ;;
