@@ -448,7 +448,8 @@ def main():
                          "(HIP events on the call's stream); the convs are >99% of it (profiles/)")
         if dtype in ("f32x3", "f16x2"):
             mac_exec = cfg["mac_row"] if cfg["mac_row"] else cfg["mac"]
-            prods = 3 if (not unet and form["kernel"] == "h2") else 6
+            # 3 partial products for the two-term fp16 kernels (the MLP's h2 kernel, the fused U-Net's P = 2 program)
+            prods = 3 if (dtype == "f16x2" and (form["fused"] if unet else form["kernel"] == "h2")) else 6
             mfma_flops = b_local * 2 * n_evals * mac_exec * 2 * prods   # bf16 / fp16 partial products per fp32 MAC
             roof = {"bound": "mfma", "achieved": mfma_flops / (kms * 1e-3) / 1e12, "peak": PEAK_BF16 / 1e12,
                     "unit": "TFLOP/s", "frac": mfma_flops / (kms * 1e-3) / PEAK_BF16,
@@ -481,7 +482,8 @@ def main():
         gemm = {"f32": "exact fp32 MFMA (v_mfma_f32_16x16x4_f32)",
                 "f32x3": "fp32-accurate split-bf16 MFMA (3 bf16 terms per operand, 6 partial products, fp32 accumulate)",
                 "f16x2": "fp32-class two-term fp16 MFMA (hi + lo fp16 per operand, weights scaled per layer by a power of "
-                         "two; 3 partial products, fp32 accumulate) for CFG-DDPM; the f32x3 kernels otherwise",
+                         "two; 3 partial products, fp32 accumulate): the MLP's CFG-DDPM kernel / the fused U-Net; the "
+                         "f32x3 kernels otherwise",
                 "f16": "fp16 operands, fp32 accumulate (v_mfma_f32_16x16x32_f16)"}[dtype]
         out = {
             "metric": "candidate trajectories/sec (100 denoise steps, H=32)" if args.workload == "cfg2" else

@@ -224,7 +224,6 @@ int check_desc(const mpcd_net_desc *d)
     for (int i = 0; i < d->n_mults; ++i)
         if (d->mults[i] < 1) return fail(MPCD_EINVAL, "bad dim_mults");
     if (d->dtype == MPCD_F16 && d->kind != MPCD_NET_UNET) return fail(MPCD_EUNSUP, "MPCD_F16 is UNet-only");
-    if (d->dtype == MPCD_F16X2 && d->kind != MPCD_NET_MLP) return fail(MPCD_EUNSUP, "MPCD_F16X2 is MLP-only");
     if (d->dtype != MPCD_F32 && d->dtype != MPCD_F32X3 && d->dtype != MPCD_F16 && d->dtype != MPCD_F16X2)
         return fail(MPCD_EINVAL, "bad dtype %d", d->dtype);
     return MPCD_OK;

@@ -5,6 +5,10 @@
 //    relative); a dot product accumulates the six partial products whose weight is >= 2^-16 of the
 //    leading one, smallest first, in fp32: fp32-level GEMM error at the bf16 rate.
 //  * P = 1 (MPCD_F16): fp16 operands, fp32 accumulation.
+//  * P = 2 (MPCD_F16X2, the fused U-Net): every operand is two fp16 terms, hi = fp16(x), lo = fp16(x - hi) (the
+//    weights scaled per conv by an exact power of two so their lo term stays a normal fp16; the accumulator is
+//    unscaled right after the GEMM); a dot product accumulates the three products lo_w hi_x, hi_w lo_x, hi_w hi_x
+//    (each dropped or residual term <= 2^-22 of |w||x|): fp32-class error at half the products of P = 3.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -32,12 +36,38 @@ MPCD_DEV uint32_t pk_f16(float lo, float hi)
 MPCD_DEV float bf_lo(uint32_t p) { return __builtin_bit_cast(float, p << 16); }
 MPCD_DEV float bf_hi(uint32_t p) { return __builtin_bit_cast(float, p & 0xffff0000u); }
 
+// v - fp32(half H of the packed fp16 pair p), exact (the remainder of a round to nearest), in one v_fma_mix_f32
+template <int H>
+MPCD_DEV float rem_f16(uint32_t p, float v)
+{
+    float r;
+    if constexpr (H == 0)
+        asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(p), "v"(v));
+    else
+        asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(p), "v"(v));
+    return r;
+}
+// two fp32 -> (hi, lo) fp16 pairs: hi = fp16(a, b), lo = fp16(a - hi, b - hi)
+MPCD_DEV void split2_pair(float a, float b, uint32_t &hi, uint32_t &lo)
+{
+    hi = pk_f16(a, b);
+    lo = pk_f16(rem_f16<0>(hi, a), rem_f16<1>(hi, b));
+}
+
 // 8 consecutive fp32 -> P planes of 8 values (16 bytes each)
 template <int P>
 MPCD_DEV void split8(const f32x4 &lo, const f32x4 &hi, u32x4 (&o)[P])
 {
     if constexpr (P == 1) {
         o[0] = u32x4{pk_f16(lo.x, lo.y), pk_f16(lo.z, lo.w), pk_f16(hi.x, hi.y), pk_f16(hi.z, hi.w)};
+    } else if constexpr (P == 2) {
+        uint32_t h[4], l[4];
+        split2_pair(lo.x, lo.y, h[0], l[0]);
+        split2_pair(lo.z, lo.w, h[1], l[1]);
+        split2_pair(hi.x, hi.y, h[2], l[2]);
+        split2_pair(hi.z, hi.w, h[3], l[3]);
+        o[0] = u32x4{h[0], h[1], h[2], h[3]};
+        o[1] = u32x4{l[0], l[1], l[2], l[3]};
     } else {
         const uint32_t a0 = pk_bf16(lo.x, lo.y), a1 = pk_bf16(lo.z, lo.w), a2 = pk_bf16(hi.x, hi.y),
                        a3 = pk_bf16(hi.z, hi.w);
@@ -59,6 +89,12 @@ MPCD_DEV void split4(const f32x4 &v, u32x2 (&o)[P])
 {
     if constexpr (P == 1) {
         o[0] = u32x2{pk_f16(v.x, v.y), pk_f16(v.z, v.w)};
+    } else if constexpr (P == 2) {
+        uint32_t h0, l0, h1, l1;
+        split2_pair(v.x, v.y, h0, l0);
+        split2_pair(v.z, v.w, h1, l1);
+        o[0] = u32x2{h0, h1};
+        o[1] = u32x2{l0, l1};
     } else {
         const uint32_t a0 = pk_bf16(v.x, v.y), a1 = pk_bf16(v.z, v.w);
         const f32x4 r = v - f32x4{bf_lo(a0), bf_hi(a0), bf_lo(a1), bf_hi(a1)};
@@ -76,6 +112,9 @@ MPCD_DEV f32x4 join4(const u32x2 (&p)[P])
 {
     if constexpr (P == 1) {
         return __builtin_convertvector(__builtin_bit_cast(f16x4, p[0]), f32x4);
+    } else if constexpr (P == 2) {
+        return __builtin_convertvector(__builtin_bit_cast(f16x4, p[0]), f32x4) +
+               __builtin_convertvector(__builtin_bit_cast(f16x4, p[1]), f32x4);
     } else {
         f32x4 v = f32x4{bf_lo(p[0].x), bf_hi(p[0].x), bf_lo(p[0].y), bf_hi(p[0].y)};
         v = v + f32x4{bf_lo(p[1].x), bf_hi(p[1].x), bf_lo(p[1].y), bf_hi(p[1].y)};
@@ -86,7 +125,7 @@ MPCD_DEV f32x4 join4(const u32x2 (&p)[P])
 template <int P>
 MPCD_DEV f32x4 mma(const u32x4 &a, const u32x4 &b, const f32x4 &c)
 {
-    if constexpr (P == 1)
+    if constexpr (P == 1 || P == 2)
         return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
                                                       0, 0);
     else
@@ -94,9 +133,15 @@ MPCD_DEV f32x4 mma(const u32x4 &a, const u32x4 &b, const f32x4 &c)
                                                        0, 0, 0);
 }
 
-// partial product i of the split: (A plane, B plane), smallest first
-constexpr int NPROD(int P) { return P == 1 ? 1 : 6; }
-template <int P> constexpr int PA(int i) { return P == 1 ? 0 : i == 0 ? 2 : i == 1 ? 1 : i == 2 ? 0 : i == 3 ? 1 : 0; }
-template <int P> constexpr int PB(int i) { return P == 1 ? 0 : i == 0 ? 0 : i == 1 ? 1 : i == 2 ? 2 : i == 3 ? 0 : i == 4 ? 1 : 0; }
+// partial product i of the split: (A plane, B plane), smallest first (P = 2: lo_w hi_x, hi_w lo_x, hi_w hi_x)
+constexpr int NPROD(int P) { return P == 1 ? 1 : P == 2 ? 3 : 6; }
+template <int P> constexpr int PA(int i)
+{
+    return P == 1 ? 0 : P == 2 ? (i == 0 ? 1 : 0) : i == 0 ? 2 : i == 1 ? 1 : i == 2 ? 0 : i == 3 ? 1 : 0;
+}
+template <int P> constexpr int PB(int i)
+{
+    return P == 1 ? 0 : P == 2 ? (i == 1 ? 1 : 0) : i == 0 ? 0 : i == 1 ? 1 : i == 2 ? 2 : i == 3 ? 0 : i == 4 ? 1 : 0;
+}
 
 }  // namespace mx

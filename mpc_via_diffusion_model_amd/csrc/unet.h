@@ -27,6 +27,9 @@ struct ConvLayer {
     const uint16_t *wmx;
     int cinp8;         // cin padded to 8 / 16 / a multiple of 32 (K per tap)
     int kc;            // k-chunks of 32 per parity
+    // two-term fp16 form (MPCD_F16X2; the fused U-Net): [parities][coutp/16][kc][2][64][8] of the weights x 1/inv2
+    const uint16_t *wmx2;
+    float inv2;        // 1 / the conv's power-of-two weight scale
 };
 
 // One fused conv launch of the bf16/f16-MFMA family (unet_mx.hip).
@@ -76,8 +79,11 @@ struct UnetWeights {
     bool ready = false;
     int n_layers = 0;
     int planes = 0;                 // 0: fp32 MFMA kernels (unet.hip); 3: split-bf16, 1: f16 (unet_mx.hip)
+    int fused_planes = 0;           // the fused program's numerics when they differ from planes (2: MPCD_F16X2)
     std::vector<ConvLayer> layers;  // in execution order (see unet.hip build_plan)
     std::shared_ptr<UnetFusedPlan> fused;  // null when the fused form does not cover the net
+    std::shared_ptr<UnetFusedPlan> fused3; // MPCD_F16X2 nets: the split-bf16 fused program, for the unclamped DDIM
+                                           // samplers (their x leaves the fp16 range)
     std::string fused_why;                 // why not (diagnostics)
 };
 
@@ -111,6 +117,7 @@ enum { UEPI_BIAS = 0, UEPI_GN_MISH = 1, UEPI_GN_MISH_COND = 2, UEPI_GN_MISH_RES 
 
 // Pack one conv for the MFMA-bf16/f16 kernels; planes = 3 (split-bf16, MPCD_F32X3) or 1 (f16, MPCD_F16).
 // w_host: conv [cout][cin][ks] or convT [cin][cout][4]. Appends to `pack` and sets L.wmx (offset), L.cinp8, L.kc.
+// planes 1 (fp16), 3 (split bf16) -> L.wmx; 2 (two-term fp16 of the weights x scale) -> L.wmx2, L.inv2 = 1 / scale
 void unet_pack_mx(int kind, int cin, int cout, int planes, const float *w_host, ConvLayer &L,
                   std::vector<uint16_t> &pack);
 // Choose rows per workgroup / tile shape and launch; kind = UCONV_*, planes 1 or 3.
@@ -139,11 +146,15 @@ struct UnetFusedStep {
     void *scratch;  // unet_fused_scratch_bytes
     uint64_t *prof;  // diagnostics: [unet_fused_prof_wgs()][n_ops][4] s_memtime stamps, or null
 };
-UnetFusedPlan *unet_fused_prepare(const mpcd_net_desc &d, const UnetWeights &W, int rows_per_wg, std::string *why);
+// planes: the program's numerics (0: the net's own - W.fused_planes, else W.planes; 3: the split-bf16 program of an
+// MPCD_F16X2 net)
+UnetFusedPlan *unet_fused_prepare(const mpcd_net_desc &d, const UnetWeights &W, int rows_per_wg, std::string *why,
+                                  int planes = 0);
 size_t unet_fused_scratch_bytes(const UnetFusedPlan &pl, int64_t batch);
 // true: the fused launch writes each branch's eps (one row per workgroup) and the CFG update runs as its own launch
 bool unet_fused_split_update(const UnetFusedPlan &pl);
 int unet_fused_rows_per_wg(const UnetFusedPlan &pl);
+int unet_fused_planes(const UnetFusedPlan &pl);
 int unet_fused_n_ops(const UnetFusedPlan &pl);
 int unet_fused_prof_wgs();
 // kind, epi, cinp, cout, lout, k-chunks, n-tiles per wave, column tiles per wave

@@ -396,10 +396,12 @@ int unet_prepare(const mpcd_net_desc &d, size_t, const TensorLookup &dev, const 
 {
     W.ready = false;
     W.layers.clear();
-    if (d.dtype != MPCD_F32 && d.dtype != MPCD_F32X3 && d.dtype != MPCD_F16)
+    if (d.dtype != MPCD_F32 && d.dtype != MPCD_F32X3 && d.dtype != MPCD_F16 && d.dtype != MPCD_F16X2)
         return uerr(MPCD_EINVAL, "UNet: bad dtype");
-    const int planes = d.dtype == MPCD_F32X3 ? 3 : d.dtype == MPCD_F16 ? 1 : 0;  // 0: fp32 MFMA kernels
-    std::vector<uint16_t> packmx;
+    // 0: fp32 MFMA kernels; MPCD_F16X2: the split-bf16 layer-by-layer kernels, the two-term fp16 fused program
+    const int planes = (d.dtype == MPCD_F32X3 || d.dtype == MPCD_F16X2) ? 3 : d.dtype == MPCD_F16 ? 1 : 0;
+    const bool h2 = d.dtype == MPCD_F16X2;
+    std::vector<uint16_t> packmx, packh2;
     if (d.horizon % (1 << (d.n_mults - 1)) != 0) return uerr(MPCD_EINVAL, "UNet: horizon must divide by 2^(levels-1)");
     const Dims m = dims_of(d);
     std::vector<float> pack;
@@ -441,6 +443,7 @@ int unet_prepare(const mpcd_net_desc &d, size_t, const TensorLookup &dev, const 
         }
         pack_conv(kind, cin, cout, wh, bd, L, pack);
         if (planes) unet_pack_mx(kind, cin, cout, planes, wh, L, packmx);
+        if (h2) unet_pack_mx(kind, cin, cout, 2, wh, L, packh2);
         L.groups = gn ? group_norm_n_groups(cout) : 1;
         L.cond_off = cond;
         L.gn_w = L.gn_b = nullptr;
@@ -482,7 +485,8 @@ int unet_prepare(const mpcd_net_desc &d, size_t, const TensorLookup &dev, const 
     if (rc) return uerr(rc, g_unet_err);
     if (planes) pack.clear();  // the mx kernels read only their own pack
     const size_t fbytes = (pack.size() * sizeof(float) + 255) / 256 * 256;
-    const size_t bytes = fbytes + packmx.size() * sizeof(uint16_t);
+    const size_t mxbytes = (packmx.size() * sizeof(uint16_t) + 255) / 256 * 256;
+    const size_t bytes = fbytes + mxbytes + packh2.size() * sizeof(uint16_t);
     if (bytes > pack_bytes) {
         if (pack_dev) (void)hipFree(pack_dev);
         pack_dev = nullptr;
@@ -495,21 +499,32 @@ int unet_prepare(const mpcd_net_desc &d, size_t, const TensorLookup &dev, const 
     if (!packmx.empty() && hipMemcpy(static_cast<char *>(pack_dev) + fbytes, packmx.data(),
                                      packmx.size() * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess)
         return uerr(MPCD_EHIP, "hipMemcpy(unet mx pack)");
+    if (!packh2.empty() && hipMemcpy(static_cast<char *>(pack_dev) + fbytes + mxbytes, packh2.data(),
+                                     packh2.size() * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess)
+        return uerr(MPCD_EHIP, "hipMemcpy(unet two-term fp16 pack)");
     for (auto &L : W.layers) {
         L.w = planes ? nullptr : static_cast<const float *>(pack_dev) + reinterpret_cast<size_t>(L.w);
         L.wmx = planes ? reinterpret_cast<const uint16_t *>(static_cast<char *>(pack_dev) + fbytes) +
                              reinterpret_cast<size_t>(L.wmx)
                        : nullptr;
+        L.wmx2 = h2 ? reinterpret_cast<const uint16_t *>(static_cast<char *>(pack_dev) + fbytes + mxbytes) +
+                          reinterpret_cast<size_t>(L.wmx2)
+                    : nullptr;
     }
     W.planes = planes;
+    W.fused_planes = h2 ? 2 : 0;
     W.n_layers = (int)W.layers.size();
     W.ready = true;
     W.fused.reset();
+    W.fused3.reset();
     W.fused_why.clear();
     // MPCD_FUSED_ROWS=<R>: the fused program with R rows per workgroup (tuning experiments; default: the first
     // instantiated configuration of the net's numerics and horizon)
     static const int fused_rows = getenv("MPCD_FUSED_ROWS") ? atoi(getenv("MPCD_FUSED_ROWS")) : 0;
     if (UnetFusedPlan *fp = unet_fused_prepare(d, W, fused_rows, &W.fused_why)) W.fused.reset(fp, unet_fused_free);
+    std::string why3;
+    if (h2)
+        if (UnetFusedPlan *fp = unet_fused_prepare(d, W, 0, &why3, 3)) W.fused3.reset(fp, unet_fused_free);
     return MPCD_OK;
 }
 
@@ -809,6 +824,13 @@ std::atomic<int> g_unet_path{0};  // mpcd_unet_force_path
 
 // the fused form runs the CFG samplers and the two-branch eps of a ConditionedTemporalUnet it covers;
 // MPCD_UNET_FUSED=0 turns it off (the layer-by-layer path then runs everything)
+// the fused program a sampler mode runs: an MPCD_F16X2 net's unclamped DDIM samplers take its split-bf16 program
+const UnetFusedPlan *fused_plan(const UnetWeights &W, int mode)
+{
+    if (W.fused_planes == 2 && (mode == MODE_DDIM_CFG || mode == MODE_DDIM)) return W.fused3.get();
+    return W.fused.get();
+}
+
 bool use_fused(const UnetWeights &W, int mode)
 {
     static const bool env_off = [] {
@@ -816,7 +838,7 @@ bool use_fused(const UnetWeights &W, int mode)
         return e && e[0] == '0';
     }();
     const int path = g_unet_path.load();
-    if (!W.fused || path == 1 || (env_off && path != 2)) return false;
+    if (!fused_plan(W, mode) || path == 1 || (env_off && path != 2)) return false;
     return mode == MODE_DDPM_CFG || mode == MODE_DDIM_CFG || mode == MODE_EPS;
 }
 }  // namespace
@@ -829,9 +851,10 @@ void unet_form(const UnetWeights &W, int mode, int32_t out[4])
 {
     const bool f = use_fused(W, mode);
     out[0] = f ? 1 : 0;
-    out[1] = W.planes;
-    out[2] = f ? unet_fused_rows_per_wg(*W.fused) : 0;
-    out[3] = f ? unet_fused_waves_per_wg(*W.fused) : 0;
+    const UnetFusedPlan *pl = fused_plan(W, mode);
+    out[1] = f ? unet_fused_planes(*pl) : W.planes;
+    out[2] = f ? unet_fused_rows_per_wg(*pl) : 0;
+    out[3] = f ? unet_fused_waves_per_wg(*pl) : 0;
 }
 
 size_t unet_workspace_bytes(const mpcd_net_desc &d, const UnetWeights &W, bool fused, int64_t batch, int nb)
@@ -840,8 +863,14 @@ size_t unet_workspace_bytes(const mpcd_net_desc &d, const UnetWeights &W, bool f
     // + the sampler state x [B][H][d] and the per-quad chain |x| maxima [B][H*d/4]
     const size_t state = sizeof(float) * ((size_t)batch * m.H * m.d + (size_t)batch * (m.H * m.d / 4 + 1));
     if (fused)  // + the eps of both branches when the update is its own launch (unet_fused_split_update)
-        return state + 256 + unet_fused_scratch_bytes(*W.fused, batch) +
-               (unet_fused_split_update(*W.fused) ? sizeof(float) * 2 * (size_t)batch * m.H * m.d + 256 : 0);
+    {
+        size_t mx = 0;  // the larger of the net's fused programs (an MPCD_F16X2 net has two)
+        for (const UnetFusedPlan *pl : {W.fused.get(), W.fused3.get()})
+            if (pl)
+                mx = std::max(mx, unet_fused_scratch_bytes(*pl, batch) +
+                                      (unet_fused_split_update(*pl) ? sizeof(float) * 2 * (size_t)batch * m.H * m.d + 256 : 0));
+        return state + 256 + mx;
+    }
     return sizeof(float) * ws_floats(m, batch * nb) + state;
 }
 
@@ -849,7 +878,7 @@ namespace {
 // the whole net + the update of one denoise step per launch (unet_fused.hip)
 int sample_fused(const mpcd_net_desc &d, const UnetWeights &W, const UnetSampleArgs &a, hipStream_t st)
 {
-    const UnetFusedPlan &pl = *W.fused;
+    const UnetFusedPlan &pl = *fused_plan(W, a.mode);
     const int flat = d.horizon * d.state_dim;
     float *xs = static_cast<float *>(a.workspace);
     uint32_t *amq = a.chain_absmax ? reinterpret_cast<uint32_t *>(xs + (size_t)a.batch * flat) : nullptr;
@@ -938,7 +967,7 @@ int unet_sample(const mpcd_net_desc &d, const UnetWeights &W, const UnetSampleAr
 {
     if (!W.ready) return uerr(MPCD_ESTATE, "UNet weights not prepared");
     if (a.fused) {
-        if (!W.fused) return uerr(MPCD_EUNSUP, "fused U-Net form requested but not prepared: " + W.fused_why);
+        if (!fused_plan(W, a.mode)) return uerr(MPCD_EUNSUP, "fused U-Net form requested but not prepared: " + W.fused_why);
         return sample_fused(d, W, a, st);
     }
     if (g_unet_path.load() == 2)  // forced fused, and unet_use_fused said no

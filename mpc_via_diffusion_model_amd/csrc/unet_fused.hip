@@ -252,7 +252,8 @@ struct ProgOf {
 struct FPtr {  // per op: weights (packed A fragments [parity][n-tile][k-chunk][plane][64][8]), bias, GroupNorm affine
     const uint16_t *w;
     const float *bias, *gnw, *gnb;
-    int32_t cond_off, pad;
+    int32_t cond_off;
+    float inv;  // P = 2: 1 / the weights' power-of-two scale (the accumulator is unscaled before the bias)
 };
 typedef const FPtr __attribute__((address_space(4))) CPtr;  // scalar loads of provably uniform values
 
@@ -618,10 +619,18 @@ MPCD_DEV void conv_op(const FArgs &a, int64_t cand0, int64_t row0, int brn, APre
 #pragma unroll
     for (int s = 0; s < U - 1; ++s)
         if (kc + s < KC) step(kc + s, s);
+    if constexpr (P == 2) {  // unscale (exact: a power of two), then the bias
+        const float inv = pp.inv;
 #pragma unroll
-    for (int j = 0; j < NTW; ++j)
+        for (int j = 0; j < NTW; ++j)
 #pragma unroll
-        for (int cc = 0; cc < NCW; ++cc) acc[j][cc] = acc[j][cc] + bias[j];
+            for (int cc = 0; cc < NCW; ++cc) acc[j][cc] = acc[j][cc] * inv + bias[j];
+    } else {
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int cc = 0; cc < NCW; ++cc) acc[j][cc] = acc[j][cc] + bias[j];
+    }
 
     if constexpr (I + 1 < N_OPS) prefetch_op<P, R, H, W, I + 1>(a, wave, lane, pre);  // lands during the epilogue
     prof_mark(a, N_OPS, I, 1);
@@ -1027,9 +1036,10 @@ struct Cfg {
 // (1, 2, 64, 4): two or three 4-wave workgroups per CU, their barriers independent (cfg5 14.7 ms per CFG evaluation
 // vs 15.3 for one 8-wave workgroup of 4 rows); the split-bf16 nets keep 4-row blocks (their weights, three planes,
 // miss the L2 per block: cfg3 3.98 ms with 2-row blocks vs 3.58)
-// (3, 1, 128, 8): the fp32-accurate Panda net (H = 128), one row per workgroup, the CFG update as its own launch
+// (3, 1, 128, 8): the fp32-accurate Panda net (H = 128), one row per workgroup, the CFG update as its own launch;
+// (2, R, H, 8): the two-term fp16 numerics (MPCD_F16X2) at the f32x3 row counts
 #define MPCD_FUSED_CFGS C_(1, 2, 64, 4) C_(3, 4, 32, 8) C_(1, 8, 32, 8) C_(3, 2, 64, 8) C_(1, 2, 128, 8) C_(3, 1, 128, 8) \
-    C_(1, 4, 64, 8) C_(1, 2, 64, 8) C_(3, 2, 32, 4)
+    C_(2, 4, 32, 8) C_(2, 2, 64, 8) C_(2, 1, 128, 8) C_(1, 4, 64, 8) C_(1, 2, 64, 8) C_(3, 2, 32, 4)
 constexpr Cfg kCfgs[] = {
 #define C_(p, r, h, w) {p, r, h, w},
     MPCD_FUSED_CFGS
@@ -1105,18 +1115,21 @@ void unet_fused_free(UnetFusedPlan *p) { delete p; }
 
 // Check the compile-time program against the loaded net and build the weight-pointer table; nullptr (and *why)
 // when the net or the numerics are not covered (the layer-by-layer path runs it instead).
-UnetFusedPlan *unet_fused_prepare(const mpcd_net_desc &d, const UnetWeights &W, int rows_per_wg, std::string *why)
+UnetFusedPlan *unet_fused_prepare(const mpcd_net_desc &d, const UnetWeights &W, int rows_per_wg, std::string *why,
+                                  int planes)
 {
     auto no = [&](const std::string &m) -> UnetFusedPlan * {
         if (why) *why = m;
         return nullptr;
     };
     if (!W.ready || W.planes == 0) return no("fused U-Net: needs the bf16 / f16 matrix-core numerics");
+    const bool h2 = planes ? planes == 2 : W.fused_planes == 2;
+    if (planes && planes != 2 && planes != W.planes) return no("fused U-Net: no pack for these numerics");
     if (!d.cfg_masked) return no("fused U-Net: the CFG net (ConditionedTemporalUnet) only");
     if (d.base_dim != 32 || d.n_mults != 3 || d.mults[0] != 1 || d.mults[1] != 2 || d.mults[2] != 4)
         return no("fused U-Net: base 32, dim_mults (1, 2, 4) only");
     if (d.state_dim < 1 || d.state_dim > 8) return no("fused U-Net: state_dim 1..8");
-    const int P = W.planes, H = d.horizon;
+    const int P = h2 ? 2 : W.planes, H = d.horizon;
     if ((H * d.state_dim) % 4) return no("fused U-Net: H*d must be a multiple of 4");
     if (W.n_layers != 35) return no("fused U-Net: unexpected layer count");
     const Prog *pg = nullptr;
@@ -1141,7 +1154,7 @@ UnetFusedPlan *unet_fused_prepare(const mpcd_net_desc &d, const UnetWeights &W, 
                            (last ? L.cout == d.state_dim && L.coutp == 16 : L.cout == o.cout && L.coutp == o.cout) &&
                            (!gn || (L.groups == kGroups && L.gn_w && L.gn_b)) && (o.epi != FE_GN_COND || L.cond_off >= 0);
         if (!match) return no("fused U-Net: layer " + std::to_string(o.layer) + " does not match the program");
-        ptrs[i] = FPtr{L.wmx, L.bias, L.gn_w, L.gn_b, L.cond_off, 0};
+        ptrs[i] = FPtr{h2 ? L.wmx2 : L.wmx, L.bias, L.gn_w, L.gn_b, L.cond_off, h2 ? L.inv2 : 1.f};
     }
     auto *pl = new UnetFusedPlan;
     pl->P = P;
@@ -1169,6 +1182,7 @@ size_t unet_fused_scratch_bytes(const UnetFusedPlan &pl, int64_t batch)
 bool unet_fused_split_update(const UnetFusedPlan &pl) { return pl.R == 1; }
 
 int unet_fused_rows_per_wg(const UnetFusedPlan &pl) { return pl.R; }
+int unet_fused_planes(const UnetFusedPlan &pl) { return pl.P; }
 int unet_fused_waves_per_wg(const UnetFusedPlan &pl) { return pl.W; }
 int unet_fused_n_ops(const UnetFusedPlan &pl) { return pl.prog->n; }
 int unet_fused_prof_wgs() { return kProfWgs; }

@@ -22,6 +22,8 @@
 // (fp64, shifted) and the elementwise epilogue, stored coalesced channels-last.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
+
 #include <atomic>
 #include <stdio.h>
 #include <stdlib.h>
@@ -884,6 +886,22 @@ void unet_pack_mx(int kind, int cin, int cout, int planes, const float *w_host, 
     const int KC = (ks * cinp + 31) / 32, npar = kind == UCONV_UP4 ? 2 : 1;
     L.cinp8 = cinp;
     L.kc = KC;
+    // planes 2: an exact power-of-two scale with max |w scale| in (2^9, 2^10], so the lo term of every weight of
+    // the conv is a normal fp16 (the fused kernel multiplies the accumulator by 1 / scale before the bias)
+    float scale = 1.f;
+    if (planes == 2) {
+        float mx = 0.f;
+        const size_t nw = (size_t)cin * cout * (kind == UCONV_UP4 ? 4 : ks);
+        for (size_t i = 0; i < nw; ++i) mx = std::max(mx, std::fabs(w_host[i]));
+        if (mx > 0.f && mx == mx) {
+            int ex;
+            std::frexp(mx, &ex);
+            int e = 10 - ex;
+            if (std::ldexp(mx, e) > 1024.f) --e;
+            scale = std::ldexp(1.f, e);
+        }
+        L.inv2 = 1.f / scale;
+    }
     const size_t base = pack.size();
     pack.resize(base + (size_t)npar * NT * KC * planes * 512, 0);
     for (int par = 0; par < npar; ++par)
@@ -907,6 +925,12 @@ void unet_pack_mx(int kind, int cin, int cout, int planes, const float *w_host, 
                         uint16_t t[3] = {0, 0, 0};
                         if (planes == 1) {
                             t[0] = f16_rne(v);
+                        } else if (planes == 2) {
+                            const float vs = v * scale;
+                            t[0] = f16_rne(vs);
+                            _Float16 h;
+                            memcpy(&h, &t[0], 2);
+                            t[1] = f16_rne(vs - (float)h);
                         } else {
                             t[0] = bf16_rne(v);
                             const float r1 = v - bf16_f(t[0]);
@@ -917,7 +941,10 @@ void unet_pack_mx(int kind, int cin, int cout, int planes, const float *w_host, 
                             pack[base + (((((size_t)par * NT + nt) * KC + kc) * planes + pl) * 64 + lane) * 8 + e] =
                                 t[pl];
                     }
-    L.wmx = reinterpret_cast<const uint16_t *>(base);  // element offset; rebased after upload
+    if (planes == 2)
+        L.wmx2 = reinterpret_cast<const uint16_t *>(base);  // element offset; rebased after upload
+    else
+        L.wmx = reinterpret_cast<const uint16_t *>(base);
 }
 
 hipError_t unet_launch_mx(int kind, int planes, ConvMK &k, hipStream_t st, std::string *why)

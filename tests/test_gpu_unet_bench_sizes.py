@@ -24,7 +24,7 @@ from ._util import assert_traj_close, make_unet, oracle_sensitivity
 pytestmark = pytest.mark.gpu
 
 MAX_CONV, MAX_BLOCK = 12, 6  # include/mpcd.h MPCD_UNET_MAX_{CONV,BLOCK}_TILINGS
-EPS_TOL = {"f32x3": 2e-5, "f16": 2e-2}
+EPS_TOL = {"f32x3": 2e-5, "f16x2": 2e-5, "f16": 2e-2}
 # BASELINE configs: (name, d, H, C, B on one GPU, dtype, schedule, N)
 CFGS = {"cfg3": (1, 32, 2, 16384, "f32x3", "exponential", 100),
         "cfg4": (1, 64, 5, 65536, "f32x3", "exponential", 100),
@@ -87,16 +87,24 @@ def test_every_tiling_bit_identical_at_bench_rows(name):
         assert torch.isfinite(gc).all() and torch.isfinite(gu).all()
 
 
-@pytest.mark.parametrize("name", sorted(CFGS))
+# the two-term fp16 fused program (MPCD_F16X2, P = 2) at the CFG-DDPM bench shapes it serves (cfg4; cfg3's unclamped
+# DDIM runs an f16x2 net's split-bf16 program)
+CFGS_H2 = {"cfg4_h2": (1, 64, 5, 65536, "f16x2", "exponential", 100)}
+
+
+@pytest.mark.parametrize("name", sorted(CFGS) + sorted(CFGS_H2))
 def test_full_batch_sampling_slice_matches_oracle(name):
     """One sample call over the whole bench batch (cfg 3: CFG-DDIM 100 steps; cfg 4: CFG-DDPM N=100
-    exponential, sqrt(1/abar - 1) up to 2.6e6; cfg 5: CFG-DDPM N=250 cosine, fp16 GEMM operands), Philox
-    noise; a slice of candidates replayed through the oracle sampler with the same draws."""
-    d, H, C, B, dtype, sched, N = CFGS[name]
+    exponential, sqrt(1/abar - 1) up to 2.6e6; cfg 5: CFG-DDPM N=250 cosine, fp16 GEMM operands; cfg4_h2: cfg 4 on
+    the two-term fp16 fused program), Philox noise; a slice of candidates replayed through the oracle sampler with the
+    same draws."""
+    d, H, C, B, dtype, sched, N = {**CFGS, **CFGS_H2}[name]
     net = make_unet(d, C, seed=11)
     plan = DiffusionMPC(NetSpec("unet", d, H, C, dtype=dtype), net.state_dict(), variance_schedule=sched,
                         n_diffusion_steps=N)
     ctx = torch.rand(1, C, generator=torch.Generator().manual_seed(5)) * 2 - 1
+    if name == "cfg4_h2":
+        assert plan.unet_form()["planes"] == 2 and plan.unet_form()["fused"]
     fn = "ddim_cfg" if name == "cfg3" else "ddpm_cfg"
     ddim_steps = N if name == "cfg3" else None
     steps = plan.n_denoise_steps(fn, 0, ddim_steps)

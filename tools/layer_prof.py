@@ -40,7 +40,8 @@ print(f"blocks {nb}: loop start us min/med/max {st.min():.1f}/{np.median(st):.1f
 print("slowest blocks (id, start, end):", [(int(i), round(float(st[i]), 1), round(float(en[i]), 1)) for i in np.argsort(-en)[:6]])
 print(f"shader clock {float(np.median(ck[:, 0] / ck[:, 1])) * 0.1:.3f} GHz (memtime / memrealtime, 8 blocks)")
 t = dbg[: 32 * 32].cpu().numpy().reshape(32, 32) / 100.0
-names = ["final+w1"] + [f"L{l}" for l in range(13)] + ["-", "tail"]
+names = (["tbl+L0"] + [f"L{l}" for l in range(1, 13)] + ["final+upd", "-", "tail"] if os.environ.get("H2") else
+         ["final+w1"] + [f"L{l}" for l in range(13)] + ["-", "tail"])
 tot = t.sum(1).mean()
 print(f"cycles/step per wave: {tot:.0f}")
 for k in range(16):

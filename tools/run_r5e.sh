@@ -1,0 +1,12 @@
+# round 5: MLP kernels after the conflict-free LDS strides - parity, lines, per-layer profile
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_mlp_h2.py tests/test_gpu_headline.py tests/test_gpu_mlp.py -x -q --timeout 300 --timeout-method thread > gpurun_out/mlp_tests.log 2>&1
+rc=$?; echo "rc=$rc" >> gpurun_out/mlp_tests.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/bench_h2.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --dtype f32x3 > gpurun_out/bench_x3.log 2>&1 || exit $?
+for b in 4096 512; do
+  MPCD_LIB=$PWD/mpc_via_diffusion_model_amd/libmpcd_prof.so DTYPE=f16x2 H2=1 B=$b timeout -k 10 300 \
+    python -u tools/layer_prof.py > gpurun_out/h2_prof_B$b.txt 2>&1 || exit $?
+done
