@@ -18,7 +18,7 @@ equal WORLD_SIZE. `--exchange gloo` rehearses the multi-rank bench with every ra
 
 The other BASELINE configs are selectable with --workload (their lines are kept under profiles/):
 cfg1 (the reference's CPU-sized case), cfg3 (pendulum, 1D U-Net, CFG-DDIM 100 steps), cfg4 (cart-pole
-NMPC dynamics, U-Net, H=64; 65536 candidates split over the ranks = strong scaling), cfg5 (12-DoF
+NMPC dynamics, U-Net, H=64, two-term fp16 fused program; 65536 candidates split over the ranks = strong scaling), cfg5 (12-DoF
 quadrotor, U-Net fp16 operands, 250 steps; 131072 candidates split over the ranks).
 """
 import argparse
@@ -49,7 +49,7 @@ WORKLOADS = {
                  ddim_steps=100, schedule="exponential", dtype="f32x3", mac=9122560 + 896 * (2 - 5), mac_row=None),
     "cfg4": dict(workload="cfg4: cart-pole (nonlinear NMPC dynamics), 1D temporal U-Net, CFG-DDPM, H=64",
                  system="cartpole_nl5", net="unet", d=1, H=64, C=5, N=100, B=65536, split=True, sampler="ddpm_cfg",
-                 ddim_steps=None, schedule="exponential", dtype="f32x3", mac=18209152, mac_row=None),
+                 ddim_steps=None, schedule="exponential", dtype="f16x2", mac=18209152, mac_row=None),
     "cfg5": dict(workload="cfg5: 12-DoF quadrotor, 1D temporal U-Net with fp16 GEMM operands, CFG-DDPM 250 steps",
                  system="quadrotor12", net="unet", d=4, H=64, C=12, N=250, B=131072, split=True, sampler="ddpm_cfg",
                  ddim_steps=None, schedule="cosine", dtype="f16", mac=18258432, mac_row=None),
@@ -179,7 +179,7 @@ def panda(args):
 
     from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec
     torch.cuda.set_device(0)
-    dtype = args.dtype or "f32x3"
+    dtype = args.dtype or "f16x2"
     sd = load_file(PANDA_CKPT)
     plan = DiffusionMPC.from_state_dict(sd, NetSpec("unet", state_dim=7, horizon=128, context_dim=20, dtype=dtype))
     rng = np.random.default_rng(1)
