@@ -117,7 +117,8 @@ struct Lds2 {
     static constexpr int CPS = BIC + COND_TOTAL * 4;
     static constexpr int BI = CPS + COND_TOTAL * 4;
     static constexpr int AMX = BI + Arch<D0>::btotal() * 4;
-    static constexpr int total = AMX + ROWS * 4;
+    static constexpr int SCL = AMX + ROWS * 4;  // the layers' scale constants (Sc: 1/s, log2(e)/s, -2/s), 3 x 16
+    static constexpr int total = SCL + 48 * 4;
     static_assert(D0 * 2 + 32 <= RS, "x planes fit a row");
     static constexpr int in_rs(int l) { return (l == 6 || l == 8) ? RS2 : RS; }
     static constexpr int in_pl(int l) { return (l == 6 || l == 8) ? PL2 : PL; }
@@ -209,7 +210,13 @@ struct MlpH2 {
     struct Sc {
         float inv, c1, k2;
     };
-    static MPCD_DEV Sc sc_of(const float *wp, int l) { return Sc{ldc(wp + 16 + l), ldc(wp + 32 + l), ldc(wp + 48 + l)}; }
+    // read from LDS (staged once): the pack's copies are constant-address scalar loads, which the compiler sinks
+    // behind each layer's opening barrier, where every layer then began with a scalar-memory round trip to L2
+    static MPCD_DEV Sc sc_of(const char *lds, int l)
+    {
+        const float *c = reinterpret_cast<const float *>(lds + L::SCL);
+        return Sc{c[l], c[16 + l], c[32 + l]};
+    }
 
     // Hidden layer l as a pipeline of passes (one n-tile x one column tile: KC chunks x 3 products); the previous
     // pass's epilogue spread as micro-steps between this pass's MFMAs, side work (loads, Philox steps) spread over
@@ -571,6 +578,7 @@ struct MlpH2 {
                 bic[cond_off(j) + i] = wp[woffh<D0>(2 * j + 1) + A::K[2 * j + 1] * A::N[2 * j + 1] + i];
         for (int i = threadIdx.x; i < COND_TOTAL; i += H2_T) cps[i] = CTX ? p.cproj[i] : 0.f;
         if (threadIdx.x < CPW) reinterpret_cast<uint32_t *>(lds + L::AMX)[threadIdx.x] = 0u;
+        if (threadIdx.x < 48) reinterpret_cast<float *>(lds + L::SCL)[threadIdx.x] = wp[16 + threadIdx.x];
         uint32_t am[2] = {0u, 0u};
         for (int i = threadIdx.x; i < CPW * QUADS; i += H2_T) {  // x_T (fp32 + planes)
             const int c = i / QUADS, qd = i - c * QUADS;
@@ -632,49 +640,49 @@ struct MlpH2 {
                 reinterpret_cast<f32x4 *>(lds + (ctx_half ? L::TPC : L::TPU))[tpi] = u * tscale;
             }
             tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 1 < p.n_steps ? s + 1 : s) * COND_TOTAL)[tpi];
-            layer_v<0>(w0, none, sc_of(ws, 0), lds, wave, lane);
+            layer_v<0>(w0, none, sc_of(lds, 0), lds, wave, lane);
             bar();
-            layer_v<1>(w1, none, sc_of(ws, 1), lds, wave, lane);
+            layer_v<1>(w1, none, sc_of(lds, 1), lds, wave, lane);
             bar();
-            layer_a<2>(w2, none, sc_of(ws, 2), lds, wave, lane);
+            layer_a<2>(w2, none, sc_of(lds, 2), lds, wave, lane);
             bar();
-            layer_a<3>(w3, none, sc_of(ws, 3), lds, wave, lane);
+            layer_a<3>(w3, none, sc_of(lds, 3), lds, wave, lane);
             bar();
-            layer_a<4>(w4, none, sc_of(ws, 4), lds, wave, lane);
+            layer_a<4>(w4, none, sc_of(lds, 4), lds, wave, lane);
             bar();
-            layer_a<5>(w5, none, sc_of(ws, 5), lds, wave, lane);
+            layer_a<5>(w5, none, sc_of(lds, 5), lds, wave, lane);
             bar();
             // the next step's Philox draw in Linear 6's MFMA slots (resident weights: the fewest live VGPRs)
             PhSt ph;
             if constexpr (STAGED_NOISE) {
                 ph_init(ph, p, s + 2, cand0, wave, lane);  // step s + 1's noise is Philox slice s + 2 (fetch_noise)
-                layer_a<6, NPH>(w6, [&](int k) { ph_step(ph, k); }, sc_of(ws, 6), lds, wave, lane);
+                layer_a<6, NPH>(w6, [&](int k) { ph_step(ph, k); }, sc_of(lds, 6), lds, wave, lane);
             } else {
-                layer_a<6>(w6, none, sc_of(ws, 6), lds, wave, lane);
+                layer_a<6>(w6, none, sc_of(lds, 6), lds, wave, lane);
             }
             bar();
             WF<8> w8;
-            layer_a<7, NFRAG<8>>(w7, [&](int k) { load_st1<8>(w8, ws, wave, lane16, k); }, sc_of(ws, 7), lds, wave, lane);
+            layer_a<7, NFRAG<8>>(w7, [&](int k) { load_st1<8>(w8, ws, wave, lane16, k); }, sc_of(lds, 7), lds, wave, lane);
             bar();
             const StepPlan cur = sp;
             if (s + 1 < p.n_steps) sp = load_plan(p.plan, s + 1);
-            layer_v<8>(w8, none, sc_of(ws, 8), lds, wave, lane);
+            layer_v<8>(w8, none, sc_of(lds, 8), lds, wave, lane);
             bar();
-            layer_v<9>(w9, none, sc_of(ws, 9), lds, wave, lane);
+            layer_v<9>(w9, none, sc_of(lds, 9), lds, wave, lane);
             bar();
-            layer_v<10, NFRAG<0>>(w10, [&](int k) { load_st1<0>(w0, ws, wave, lane16, k); }, sc_of(ws, 10), lds, wave, lane);
+            layer_v<10, NFRAG<0>>(w10, [&](int k) { load_st1<0>(w0, ws, wave, lane16, k); }, sc_of(lds, 10), lds, wave, lane);
             f32x4 nzc[NZT];
 #pragma unroll
             for (int j = 0; j < NZT; ++j) nzc[j] = nz[j];
             if (STAGED_NOISE && s + 1 < p.n_steps) ph_take(nz, ph, sp, cand0, p, wave, lane);
             else if (s + 1 < p.n_steps) fetch_noise(nz, p, sp, s + 1, cand0, wave, lane);
             bar();
-            layer_v<11, NFRAG<13>>(w11, [&](int k) { load_st1<13>(w13, ws, wave, lane16, k); }, sc_of(ws, 11), lds, wave,
+            layer_v<11, NFRAG<13>>(w11, [&](int k) { load_st1<13>(w13, ws, wave, lane16, k); }, sc_of(lds, 11), lds, wave,
                                    lane);
             bar();
-            layer_v<12>(w12, none, sc_of(ws, 12), lds, wave, lane);
+            layer_v<12>(w12, none, sc_of(lds, 12), lds, wave, lane);
             bar();
-            final_and_update(w13, sc_of(ws, 13), lds, p, cur, s, cand0, nzc, am, wave, lane);
+            final_and_update(w13, sc_of(lds, 13), lds, p, cur, s, cand0, nzc, am, wave, lane);
             bar();  // x planes of the next step written; this step's last reads of TPC / TPU long done
         }
 #ifdef MPCD_PROF_LAYERS
