@@ -13,7 +13,7 @@ ap.add_argument("--N", type=int, default=100)
 ap.add_argument("--steps", type=int, default=10, help="DDIM sampling steps (network evaluations)")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--schedule", default="exponential")
-ap.add_argument("--dtype", default="f32x3", choices=["f32", "f32x3", "f16"])
+ap.add_argument("--dtype", default="f32x3", choices=["f32", "f32x3", "f16", "f16x2"])
 ap.add_argument("--fuse", default="", help="MPCD_UNET_FUSE (0 never, 1 always, empty: measured)")
 ap.add_argument("--path", default="auto", choices=["auto", "layered", "fused"], help="mpcd_unet_force_path")
 a = ap.parse_args()

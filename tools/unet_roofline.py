@@ -7,7 +7,7 @@ on the fused path, or the period of the conv launch sequence (it repeats once th
 picks) layer by layer - and per launch reports duration, HBM bytes (2 x FETCH_SIZE +
 WRITE_SIZE, x1024: on gfx950 FETCH_SIZE tallies half the bytes of 16-B/lane streaming reads,
 MI355X_MICROARCH.md §HBM) and MFMA busy; per forward the SURVEY §8d algorithmic FLOPs (2 x MAC x rows),
-the executed matrix-core FLOPs (x6 for the split-bf16 net), and the fractions of the MFMA and HBM peaks.
+the executed matrix-core FLOPs (x6 for the split-bf16 net, x3 for the two-term fp16 one), and the fractions of the MFMA and HBM peaks.
 """
 import csv
 import json
@@ -74,10 +74,10 @@ def main(cfg, B, H, d, C, dtype, out=None):
         for j, s in enumerate(seq[-p:]):
             assert s["name"] == names[-p + j]
             ctr.setdefault(j, {}).update({k: v for k, v in s.items() if k != "name"})
-    planes = 3 if dtype == "f32x3" else 1
+    prods = {"f32x3": 6, "f16x2": 3}.get(dtype, 1)  # partial products per fp32 MAC on the matrix cores
     rows_n = 2 * B
     flop_alg = 2.0 * mac_fwd(H, d, C) * rows_n
-    flop_exec = flop_alg * (6 if planes == 3 else 1)
+    flop_exec = flop_alg * prods
     t = sum(dur)
     hbm = [(2 * ctr[j].get("FETCH_SIZE", 0) + ctr[j].get("WRITE_SIZE", 0)) * 1024 for j in range(p)]
     # SQ_VALU_MFMA_BUSY_CYCLES = 16 cycles per 16x16x32 MFMA summed over all SIMDs (checked against SQ_INSTS_MFMA)
