@@ -41,13 +41,13 @@ def _disassemble(tmp_path):
 
 
 def test_every_kernel_keeps_packed_reads_of_transcendentals_two_wait_states_away(tmp_path):
-    """Every kernel of the shipped code object: the MLP samplers (mlp_rw_kernel is the cfg2 headline kernel; the
-    streaming mlp_x3_kernel and the exact-fp32 mlp_sample_kernel), the layer-by-layer and fused U-Nets, the prologues,
-    the rollout and the training kernels."""
+    """Every kernel of the shipped code object: the MLP samplers (mlp_h2_kernel, the cfg1 / cfg2 headline kernel; the
+    split-bf16 mlp_rw_kernel and mlp_x3_kernel, the exact-fp32 mlp_sample_kernel), the layer-by-layer and fused
+    U-Nets, the prologues, the rollout and the training kernels."""
     import trans_hazard as th
     sites = th.scan(_disassemble(tmp_path))
     kernels = {s[0] for s in sites if s[0]}
-    for k in ("unet_fused_kernel", "conv_mx_kernel", "mlp_rw_kernel", "mlp_x3_kernel", "mlp_sample_kernel"):
+    for k in ("unet_fused_kernel", "conv_mx_kernel", "mlp_h2_kernel", "mlp_rw_kernel", "mlp_x3_kernel", "mlp_sample_kernel"):
         assert any(k in n for n in kernels), f"{k} not found in the code object"
     packed = [s for s in sites if s[4]]
     close = [s for s in packed if s[3] < 2]
@@ -58,11 +58,13 @@ def test_every_kernel_keeps_packed_reads_of_transcendentals_two_wait_states_away
 
 
 def test_every_mfma_source_two_wait_states_after_a_valu_write(tmp_path):
-    """csrc/mlp_rw.hip issues MFMAs with AGPR weight operands as inline asm, which the compiler's hazard pass does
-    not treat as MFMAs: no MFMA of the library may read a register a VALU op wrote under 2 wait states before."""
+    """csrc/mlp_rw.hip and csrc/mlp_h2.hip issue MFMAs with AGPR weight operands as inline asm, which the compiler's
+    hazard pass does not treat as MFMAs: no MFMA of the library may read a register a VALU op wrote under 2 wait
+    states before."""
     import mfma_hazard as mh
     lines = _disassemble(tmp_path)
-    assert any("mlp_rw_kernel" in ln for ln in lines), "mlp_rw_kernel not found in the code object"
+    for k in ("mlp_rw_kernel", "mlp_h2_kernel"):
+        assert any(k in ln for ln in lines), f"{k} not found in the code object"
     assert any("v_mfma" in ln and ", a[" in ln for ln in lines), "no MFMA with AGPR operands (resident weights?)"
     bad = mh.scan(lines)
     assert not bad, f"{len(bad)} MFMA sources written by a VALU op under 2 wait states: {bad[:3]}"
