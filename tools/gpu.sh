@@ -25,7 +25,7 @@ mkdir -p gpurun_out/prof gpurun_out/uroof
 declare -A UARGS=(
   [cfg3]="--B 16384 --H 32 --d 1 --C 2 --N 100 --dtype f32x3"
   [cfg4]="--B 65536 --H 64 --d 1 --C 5 --N 100 --dtype f32x3"
-  [cfg4h]="--B 65536 --H 64 --d 1 --C 5 --N 100 --dtype f16x2"
+  [cfg4h]="--B 65536 --H 64 --d 1 --C 5 --N 4 --schedule cosine --sampler ddpm_cfg --dtype f16x2"
   [cfg5]="--B 131072 --H 64 --d 4 --C 12 --N 250 --schedule cosine --dtype f16"
 )
 
