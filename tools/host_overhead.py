@@ -18,7 +18,7 @@ from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec, systems  # noqa: 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 cfg = bench.WORKLOADS["cfg2"]
 torch.cuda.set_device(0)
-spec = NetSpec("mlp", state_dim=cfg["d"], horizon=cfg["H"], context_dim=cfg["C"], dtype="f32x3")
+spec = NetSpec("mlp", state_dim=cfg["d"], horizon=cfg["H"], context_dim=cfg["C"], dtype=cfg["dtype"])
 plan = DiffusionMPC(spec, bench.synthetic_params(spec, seed=0), variance_schedule=cfg["schedule"], n_diffusion_steps=cfg["N"])
 system = systems.get(cfg["system"])
 x0s = np.random.default_rng(1).uniform(-1, 1, (400, system.n_x))
