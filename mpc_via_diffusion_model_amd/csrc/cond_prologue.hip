@@ -16,6 +16,7 @@
 namespace {
 
 constexpr int TDIM = 32;    // SinusoidalPosEmb / time_emb_dim
+static_assert(TDIM == kCondTdim, "ctx_proj_col's time columns");
 constexpr int THID = 128;   // TimeEncoder hidden = 4 * 32
 
 __global__ __launch_bounds__(128) void time_prologue_kernel(const StepPlan *plan, const float *w1, const float *b1,
@@ -81,13 +82,7 @@ __global__ __launch_bounds__(256) void ctx_prologue_row_kernel(const CtxRowArg r
 {
     const int col = blockIdx.x * blockDim.x + threadIdx.x;
     if (col >= cond_total) return;
-    int l = 0;
-    while (l + 1 < n_layers && layers[l + 1].off <= col) ++l;
-    const CondLayer L = layers[l];
-    const int n = col - L.off;
-    double acc = 0.0;
-    for (int k = 0; k < ctx_dim; ++k) acc += (double)L.W[(size_t)n * cond_dim + TDIM + k] * (double)mish_precise(row.v[k]);
-    cproj[col] = (float)acc;
+    cproj[col] = ctx_proj_col(row, ctx_dim, layers, n_layers, cond_dim, col);
 }
 
 }  // namespace

@@ -30,6 +30,21 @@ constexpr int kCtxRowMax = 64;
 struct CtxRowArg {
     float v[kCtxRowMax];
 };
+constexpr int kCondTdim = 32;  // time_emb_dim: the cond Linears' first input columns (cond_prologue.hip TDIM)
+// Column col of one shared context row's projection, cond_mlp_j.W[n, T:] . Mish(ctx) in fp64: the body of
+// ctx_prologue_row_kernel, and of the fp16 MLP kernel's in-launch form (mpcd_mpc_step), so both give the same bits
+MPCD_DEV float ctx_proj_col(const CtxRowArg &row, int ctx_dim, const CondLayer *layers, int n_layers, int cond_dim,
+                            int col)
+{
+    int l = 0;
+    while (l + 1 < n_layers && layers[l + 1].off <= col) ++l;
+    const CondLayer L = layers[l];
+    const int n = col - L.off;
+    double acc = 0.0;
+    for (int k = 0; k < ctx_dim; ++k)
+        acc += (double)L.W[(size_t)n * cond_dim + kCondTdim + k] * (double)mish_precise(row.v[k]);
+    return (float)acc;
+}
 void launch_ctx_prologue_row(const CtxRowArg &row, int ctx_dim, const CondLayer *layers_dev, int n_layers,
                              int cond_dim, int cond_total, float *cproj, hipStream_t stream);
 
@@ -76,6 +91,12 @@ struct MlpSampleArgs {
     int32_t clamp_x0;
     float wp1, wf;           // fp32(1 + w), fp32(w)
     float *dbg;              // debug: block 0 dumps every layer output [14][32][256] (null in production)
+    // mpcd_mpc_step with the fp16 kernel: the shared context row's projection computed in the launch (cps staging)
+    // instead of read from cproj (no ctx prologue launch); cproj still non-null (selects the ctx instantiation)
+    int32_t ctx_fused;
+    int32_t ctx_dim, n_cond, cond_dim;
+    const CondLayer *cond_layers;
+    CtxRowArg ctx_row;
 };
 
 int mlp_packed_floats(int d0);

@@ -576,7 +576,10 @@ struct MlpH2 {
         for (int j = 0; j < 6; ++j)
             for (int i = threadIdx.x; i < A::N[2 * j + 1]; i += H2_T)
                 bic[cond_off(j) + i] = wp[woffh<D0>(2 * j + 1) + A::K[2 * j + 1] * A::N[2 * j + 1] + i];
-        for (int i = threadIdx.x; i < COND_TOTAL; i += H2_T) cps[i] = CTX ? p.cproj[i] : 0.f;
+        for (int i = threadIdx.x; i < COND_TOTAL; i += H2_T)
+            cps[i] = !CTX ? 0.f
+                          : p.ctx_fused ? ctx_proj_col(p.ctx_row, p.ctx_dim, p.cond_layers, p.n_cond, p.cond_dim, i)
+                                        : p.cproj[i];
         if (threadIdx.x < CPW) reinterpret_cast<uint32_t *>(lds + L::AMX)[threadIdx.x] = 0u;
         if (threadIdx.x < 48) reinterpret_cast<float *>(lds + L::SCL)[threadIdx.x] = wp[16 + threadIdx.x];
         uint32_t am[2] = {0u, 0u};

@@ -657,11 +657,14 @@ static int sample_impl(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr,
     }
     const float *cproj = nullptr;
     int64_t cstride = 0;
+    const bool fuse_ctx = ctx_row && d.kind == MPCD_NET_MLP && mlp_kernel_of(c, a->sampler, true) == MLPK_H2;
     if (d.context_dim > 0) {
         const bool shared = ctx_row || a->context_shared;
         const int64_t rows = shared ? 1 : a->batch;
         if ((rc = c->cproj.ensure(sizeof(float) * (size_t)rows * c->cond_total))) return rc;
-        if (ctx_row)
+        if (fuse_ctx) {
+            // the fp16 MLP kernel computes the row's projection in its own staging: one launch fewer
+        } else if (ctx_row)
             launch_ctx_prologue_row(*ctx_row, d.context_dim, cl, c->n_cond, c->cond_dim, c->cond_total,
                                     c->cproj.as<float>(), st);
         else
@@ -693,6 +696,14 @@ static int sample_impl(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr,
         m.clamp_x0 = a->clamp_x0;
         m.wp1 = wp1;
         m.wf = wf;
+        if (fuse_ctx) {
+            m.ctx_fused = 1;
+            m.ctx_row = *ctx_row;
+            m.ctx_dim = d.context_dim;
+            m.cond_layers = cl;
+            m.n_cond = c->n_cond;
+            m.cond_dim = c->cond_dim;
+        }
         HIP_TRY(launch_mlp(c, m, cfg ? 2 : 1, st));
     } else {
         UnetSampleArgs u{};

@@ -134,13 +134,16 @@ def test_mpc_step_matches_oracle_pipeline(native, B):
 
 @pytest.mark.parametrize("B", [64, 1000, 4096 + 17])
 @pytest.mark.parametrize("sample_fn", ["ddpm_cfg", "ddim_cfg"])
-def test_native_step_equals_composed_step(B, sample_fn):
+@pytest.mark.parametrize("dtype", ["f32x3", "f16x2"])
+def test_native_step_equals_composed_step(B, sample_fn, dtype):
     """mpcd_mpc_step (one call, fused select) gives bit-identical samples, costs, winner and trajectory
     to the step composed from sample / clip flag / rollout / argmin / unnormalise; ragged B included
-    (the last rollout workgroup is partial). DDIM leaves the clip flag live (no provable bound)."""
+    (the last rollout workgroup is partial). DDIM leaves the clip flag live (no provable bound). f16x2 DDPM: the
+    fp16 kernel computes the context row's projection inside its launch (no ctx prologue) and must match the
+    composed step, which runs the prologue kernel."""
     d, H, C = 2, 32, 4
     net = make_mlp(d, H, C, seed=5)
-    plan = DiffusionMPC(NetSpec("mlp", d, H, C), net.state_dict(), n_diffusion_steps=25,
+    plan = DiffusionMPC(NetSpec("mlp", d, H, C, dtype=dtype), net.state_dict(), n_diffusion_steps=25,
                         action_limits=(np.array([-2.0, -0.5]), np.array([2.0, 0.5])))
     x0 = np.array([0.4, -0.3, 0.2, -0.1])
     sysm = systems.double_int2d()

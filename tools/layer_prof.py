@@ -40,7 +40,10 @@ print(f"blocks {nb}: loop start us min/med/max {st.min():.1f}/{np.median(st):.1f
 print("slowest blocks (id, start, end):", [(int(i), round(float(st[i]), 1), round(float(en[i]), 1)) for i in np.argsort(-en)[:6]])
 print(f"shader clock {float(np.median(ck[:, 0] / ck[:, 1])) * 0.1:.3f} GHz (memtime / memrealtime, 8 blocks)")
 t = dbg[: 32 * 32].cpu().numpy().reshape(32, 32) / 100.0
-names = (["tbl+L0"] + [f"L{l}" for l in range(1, 13)] + ["final+upd", "-", "tail"] if os.environ.get("H2") else
+# segment k accumulates the barrier-to-barrier spans that end at the k-th barrier of a step; the staging barrier
+# before the loop takes index 0, so a step's first span (the cond tables + Linear 0) lands in index 1 and its last
+# (the final Linear + update) in index 0
+names = (["final+upd", "tbl+L0"] + [f"L{l}" for l in range(1, 13)] + ["-", "tail"] if os.environ.get("H2") else
          ["final+w1"] + [f"L{l}" for l in range(13)] + ["-", "tail"])
 tot = t.sum(1).mean()
 print(f"cycles/step per wave: {tot:.0f}")
