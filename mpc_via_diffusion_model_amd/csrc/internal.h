@@ -131,5 +131,11 @@ struct RolloutSelect {
     // clip_flag_kernel test; a small batch's per-candidate chain maxima) instead of read from flag_dev
     const float *clip_src;
     int64_t clip_n;
+    // optional: the result block {best, winner row, clip code} (step_out's layout) also written by the selecting
+    // workgroup to mapped host memory, then *host_flag = host_seq after a system-scope fence: mpcd_mpc_step spins
+    // on that word instead of a device-to-host copy and a stream synchronisation
+    char *host_out;
+    uint32_t *host_flag;
+    uint32_t host_seq;
 };
 constexpr int kRolloutBlock = 64;  // candidates per rollout workgroup

@@ -291,7 +291,9 @@ struct mpcd_ctx {
     // and its pinned host mirror (one D2H copy per control step)
     DevBuf step_ctx, step_part, step_out, step_amax;
     void *step_host = nullptr;
+    void *step_host_dev = nullptr;  // step_host's device address (mapped pinned memory)
     size_t step_host_bytes = 0;
+    uint32_t step_seq = 0;          // completion word value of the last single-rank mpcd_mpc_step
     int32_t step_flags = 0;  // mpcd_last_step_flags
 };
 
@@ -1143,12 +1145,17 @@ int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, fl
     // host staging (pinned): [context row | result block]
     // result block: {best, winner row [row] fp32, clip code int32} - one D2H copy
     const size_t out_bytes = sizeof(mpcd_best) + sizeof(float) * (size_t)row + sizeof(int32_t);
-    const size_t host_bytes = 64 + out_bytes;
+    const size_t flag_off = 64 + ((out_bytes + 63) & ~(size_t)63);  // the completion word, own 64-byte line
+    const size_t host_bytes = flag_off + 64;
     if (c->step_host_bytes < host_bytes) {
         if (c->step_host) (void)hipHostFree(c->step_host);
         c->step_host = nullptr;
+        c->step_host_dev = nullptr;
         c->step_host_bytes = 0;
         HIP_TRY(hipHostMalloc(&c->step_host, host_bytes, hipHostMallocDefault));
+        HIP_TRY(hipHostGetDevicePointer(&c->step_host_dev, c->step_host, 0));
+        memset(c->step_host, 0, host_bytes);
+        c->step_seq = 0;
         c->step_host_bytes = host_bytes;
     }
     if ((rc = c->step_ctx.ensure(64)) || (rc = c->step_out.ensure(out_bytes))) return rc;
@@ -1201,9 +1208,16 @@ int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, fl
     double *part_cost = c->step_part.as<double>();
     int64_t *part_idx = reinterpret_cast<int64_t *>(part_cost + n_part);
     int32_t *code_dev = reinterpret_cast<int32_t *>(u_dev + row);
+    void *host_out = static_cast<char *>(c->step_host) + 64;
+    volatile uint32_t *host_flag = reinterpret_cast<volatile uint32_t *>(static_cast<char *>(c->step_host) + flag_off);
+    uint32_t seq = 0;
     if (!c->comm) {  // rollout + cost + argmin + the winner's unnormalised row + the clip code in one launch
+        seq = ++c->step_seq;
+        if (seq == 0) seq = ++c->step_seq;
+        char *hdev = static_cast<char *>(c->step_host_dev);
         RolloutSelect sel{best_dev, u_dev,    part_cost, part_idx, c->sync_ws() + 8, n_part, sa.global_offset, code_dev,
-                          fuse_clip ? clip_src : nullptr, fuse_clip ? clip_n : 0};
+                          fuse_clip ? clip_src : nullptr, fuse_clip ? clip_n : 0, hdev + 64,
+                          reinterpret_cast<uint32_t *>(hdev + flag_off), seq};
         HIP_TRY(launch_rollout_cost(sys, a->x0, nullptr, B, sa.x_out, a->act_min, a->act_max, flag, B, H,
                                     a->cost_local, st, &sel));
     } else {
@@ -1217,9 +1231,24 @@ int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, fl
         HIP_TRY(launch_unnormalize(row_norm, row, d.state_dim, flag, a->act_min, a->act_max, u_dev, st));
         HIP_TRY(hipMemcpyAsync(code_dev, flag, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     }
-    void *host_out = static_cast<char *>(c->step_host) + 64;
-    HIP_TRY(hipMemcpyAsync(host_out, c->step_out.p, out_bytes, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    if (c->comm) {
+        HIP_TRY(hipMemcpyAsync(host_out, c->step_out.p, out_bytes, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    } else {
+        // the selecting workgroup wrote the block to mapped host memory and then the completion word: spin on it
+        // (no copy launch, no stream synchronisation wake-up); the stream is queried now and then so that a failed
+        // launch cannot leave this loop waiting
+        for (uint32_t n = 1; *host_flag != seq; ++n) {
+            if ((n & 4095) == 0) {
+                const hipError_t q = hipStreamQuery(st);
+                if (q == hipSuccess && *host_flag != seq)
+                    return fail(MPCD_EHIP, "mpcd_mpc_step: the stream finished without the result block");
+                if (q != hipSuccess && q != hipErrorNotReady) HIP_TRY(q);
+            }
+            __builtin_ia32_pause();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    }
     memcpy(best_host, host_out, sizeof(mpcd_best));
     memcpy(u_best_host, static_cast<char *>(host_out) + sizeof(mpcd_best), sizeof(float) * (size_t)row);
     int32_t code = 0;

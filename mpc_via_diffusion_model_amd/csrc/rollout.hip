@@ -44,6 +44,9 @@ struct SelectK {
     int32_t *code_out;   // optional: flags[0] copied next to the winner (saves the caller a device copy)
     const float *clip_src;  // optional: the clip code computed here over clip_src[0, clip_n) (RolloutSelect)
     int64_t clip_n;
+    char *host_out;         // optional: the result block mirrored to mapped host memory + a completion word
+    uint32_t *host_flag;
+    uint32_t host_seq;
 };
 
 // (v, i) beats (bv, bi): NaN = +inf, lower cost, then lower index; i < 0 = empty
@@ -227,11 +230,26 @@ __global__ __launch_bounds__(RT_THREADS) void rollout_cost_kernel(const SysK S, 
     const int64_t nvalid = min((int64_t)RT_THREADS, batch - c0);
     const float *src = u_norm + (size_t)c0 * row;
     if ((row & 3) == 0) {  // 16-byte loads (a row never straddles a quad)
-        for (int i = threadIdx.x; i < nvalid * row / 4; i += RT_THREADS) {
-            const f32x4 v = ldg4(src + 4 * i);
-            const int c = 4 * i / row, k = 4 * i - c * row;
+        // in batches of UNR loads per lane, all issued before the first LDS store: one memory latency per batch
+        // (a load -> store loop waits for every load in turn: 16 latencies at H = 32, nu = 2)
+        constexpr int UNR = 8;
+        const int nq = (int)(nvalid * row / 4);
+        for (int base = 0; base < nq; base += UNR * RT_THREADS) {
+            f32x4 v[UNR];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) su[c * stride + k + e] = v[e];
+            for (int u = 0; u < UNR; ++u) {
+                const int i = base + u * RT_THREADS + (int)threadIdx.x;
+                v[u] = i < nq ? ldg4(src + 4 * i) : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const int i = base + u * RT_THREADS + (int)threadIdx.x;
+                if (i < nq) {
+                    const int c = 4 * i / row, k = 4 * i - c * row;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) su[c * stride + k + e] = v[u][e];
+                }
+            }
         }
     } else {
         for (int i = threadIdx.x; i < nvalid * row; i += RT_THREADS) {
@@ -323,16 +341,30 @@ __global__ __launch_bounds__(RT_THREADS) void rollout_cost_kernel(const SysK S, 
             if (better(pv, pi, v, i)) { v = pv; i = pi; }
         }
         wave_argmin(v, i);
+        const int32_t ccode = K.clip_src ? code : flags[0];
+        float *hrow = K.host_out ? reinterpret_cast<float *>(K.host_out + sizeof(mpcd_best)) : nullptr;
         if (threadIdx.x == 0) {
-            K.best->cost = v;
-            K.best->index = i < 0 ? -1 : K.offset + i;
+            const mpcd_best bst{v, i < 0 ? -1 : K.offset + i};
+            *K.best = bst;
             *K.counter = 0u;
-            if (K.code_out) *K.code_out = K.clip_src ? code : flags[0];
+            if (K.code_out) *K.code_out = ccode;
+            if (hrow) {
+                *reinterpret_cast<mpcd_best *>(K.host_out) = bst;
+                *reinterpret_cast<int32_t *>(hrow + row) = ccode;
+            }
         }
         if (i >= 0 && K.row_out) {
             const bool clip0 = K.clip_src ? code == 1 : flags[0] == 1;
-            for (int k = threadIdx.x; k < row; k += RT_THREADS)
-                K.row_out[k] = unnorm1(u_norm[(size_t)i * row + k], clip0, S.umin[k % nu], S.umax[k % nu]);
+            for (int k = threadIdx.x; k < row; k += RT_THREADS) {
+                const float o = unnorm1(u_norm[(size_t)i * row + k], clip0, S.umin[k % nu], S.umax[k % nu]);
+                K.row_out[k] = o;
+                if (hrow) hrow[k] = o;
+            }
+        }
+        if (hrow) {  // every lane's host stores ordered before the completion word
+            __threadfence_system();
+            __syncthreads();
+            if (threadIdx.x == 0) __hip_atomic_store(K.host_flag, K.host_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
@@ -532,8 +564,8 @@ hipError_t launch_rollout_cost(const mpcd_system_desc &d, const double *x0_host,
     SelectK K = {};
     if (sel) {
         if (group != batch || sel->n_part < (batch + RT_THREADS - 1) / RT_THREADS) return hipErrorInvalidValue;
-        K = SelectK{sel->best,   sel->row_out, sel->part_cost, sel->part_idx, sel->counter,
-                    sel->offset, sel->code_out, sel->clip_src,  sel->clip_n};
+        K = SelectK{sel->best,   sel->row_out, sel->part_cost, sel->part_idx, sel->counter,   sel->offset,
+                    sel->code_out, sel->clip_src, sel->clip_n,   sel->host_out, sel->host_flag, sel->host_seq};
     }
     const dim3 grid((unsigned)((batch + RT_THREADS - 1) / RT_THREADS));
 #define MPCD_ROLLOUT(SYS_)                                                                                          \
