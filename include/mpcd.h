@@ -295,8 +295,11 @@ int mpcd_select(mpcd_ctx *ctx, const double *cost_local, int64_t n_local, const 
 /* ---- One control step in one call: the whole per-step path of Diffusion_MPC_Inference.py:229-262 /
  * Cart_Diffusion_inference.py:439-470 (normalize_condition -> run_CFG -> unnormalize_states -> cost of
  * every candidate -> argmin -> applied action) for this rank's shard, plus the exchange of mpcd_select
- * when the context has a communicator. Everything stays on the device until one D2H copy of the
- * result; the call then synchronises the stream, so best_host / u_best_host are valid on return. */
+ * when the context has a communicator. Everything stays on the device until the result block leaves it: on one
+ * rank the selecting rollout workgroup writes it to mapped pinned host memory followed by a completion word the
+ * call spins on (no copy launch, no stream-synchronisation wake-up; every kernel's device writes precede that
+ * word); with a communicator one D2H copy and a stream synchronisation. best_host / u_best_host are valid on
+ * return either way. */
 /* The reference scripts call run_CFG(..., return_chain=True) and unnormalise the WHOLE chain
  * (Cart_Diffusion_inference.py:450-463, Diffusion_MPC_Inference.py:232-247), so the clip test sees x_T
  * ~ N(0, 1) as well and practically always clips. MPCD_CLIP_CHAIN reproduces that (the default);

@@ -509,7 +509,8 @@ class DiffusionMPC:
     def _mpc_step_native(self, x0, system, n_samples, w, sample_fn, n_wo_noise, ddim_steps, clamp_x0, seed, noise,
                          comm, clip_rule="chain"):
         """mpc_step as one libmpcd call (mpcd_mpc_step): one H2D copy of the context row, the kernels,
-        one D2H copy of {best, u_best}, one stream synchronisation."""
+        the result block {best, u_best} written to pinned host memory by the selecting workgroup (one rank) or one
+        D2H copy + stream synchronisation (with a communicator)."""
         size, rank = (comm.size, comm.rank) if comm is not None else (1, 0)
         B, H, d = int(n_samples), self.spec.horizon, self.spec.state_dim
         if d != system.n_u:
