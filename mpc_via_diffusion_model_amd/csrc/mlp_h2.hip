@@ -120,6 +120,13 @@ struct Lds2 {
     static constexpr int SCL = AMX + ROWS * 4;  // the layers' scale constants (Sc: 1/s, log2(e)/s, -2/s), 3 x 16
     static constexpr int total = SCL + 48 * 4;
     static_assert(D0 * 2 + 32 <= RS, "x planes fit a row");
+    // Row swizzle of every activation plane: in rows with bit 2 set the 16-byte units are swapped in pairs (byte
+    // offset b -> b ^ 16). The B-fragment reads (ds_read_b128 of whole units) stay conflict-free; the epilogue's
+    // ds_write_b64 of 16 rows at one feature offset (one lane group, banks mod 32) drop from 4-way to 2-way bank
+    // conflicts (16 rows on the 8 unit positions of 128 bytes: 2-way is that pattern's floor). In lane terms: a
+    // B-fragment read of quarter q takes unit q ^ s, an epilogue store of quarter q writes at 8 (q ^ 2s), with
+    // s = bit 2 of the lane's row (= bit 2 of its column in every layout here).
+    static MPCD_DEV int swz(int r) { return (r >> 2) & 1; }
     static constexpr int in_rs(int l) { return (l == 6 || l == 8) ? RS2 : RS; }
     static constexpr int in_pl(int l) { return (l == 6 || l == 8) ? PL2 : PL; }
     static constexpr int out_rs(int l) { return (l == 5 || l == 7) ? RS2 : RS; }
@@ -247,7 +254,7 @@ struct MlpH2 {
         auto ldx = [&](u32x4 (&x)[2], int i) {  // step i = (pass i / KC, k-chunk i % KC)
             const int p = i / KC, kc = i % KC, ct = ct_of<l>(wave, cp(p));
             const int row = in_shared ? cand_of(ct, col) : ct * 16 + col;
-            const char *b = lds + in_off(l) + row * L::in_rs(l) + (kc * 32 + 8 * q) * 2;
+            const char *b = lds + in_off(l) + row * L::in_rs(l) + kc * 64 + 16 * (q ^ L::swz(row));
             x[0] = *reinterpret_cast<const u32x4 *>(b);
             x[1] = *reinterpret_cast<const u32x4 *>(b + L::in_pl(l));
         };
@@ -278,7 +285,8 @@ struct MlpH2 {
                 return;
             }
             const int n = nt_of<l>(wave, jp(p)) * 16 + 4 * q;
-            char *o = lds + out_off(l) + (ct_of<l>(wave, cp(p)) * 16 + col) * L::out_rs(l) + n * 2;
+            const int ro = ct_of<l>(wave, cp(p)) * 16 + col;
+            char *o = lds + out_off(l) + ro * L::out_rs(l) + (n * 2 - 8 * q) + 8 * (q ^ (L::swz(ro) << 1));
             switch (k - NEPI) {
             case 0: h01 = pk_f16(ev.x, ev.y); h23 = pk_f16(ev.z, ev.w); break;
             case 1: r0 = rem_f16<0>(h01, ev.x); r1 = rem_f16<1>(h01, ev.y); break;
@@ -345,7 +353,7 @@ struct MlpH2 {
         *reinterpret_cast<f32x4 *>(lds + L::XB + (cl * L::SX + n) * 4) = x;
         u32x2 hi, lo;
         split2(x, hi, lo);
-        char *o = lds + L::S1 + cl * L::RS + n * 2;
+        char *o = lds + L::S1 + cl * L::RS + ((n * 2) ^ (L::swz(cl) << 4));
         *reinterpret_cast<u32x2 *>(o) = hi;
         *reinterpret_cast<u32x2 *>(o + L::PL) = lo;
     }
@@ -367,7 +375,7 @@ struct MlpH2 {
         }
 #pragma unroll
         for (int c = 0; c < NCT; ++c) {
-            const char *b = lds + L::T1 + (c * 16 + col) * L::RS + 8 * q * 2;
+            const char *b = lds + L::T1 + (c * 16 + col) * L::RS + 16 * (q ^ L::swz(col));
             u32x4 x[2];
             x[0] = *reinterpret_cast<const u32x4 *>(b);
             x[1] = *reinterpret_cast<const u32x4 *>(b + L::PL);
