@@ -465,7 +465,7 @@ struct MlpH2 {
     // The next step's Philox draw as NPH micro-steps (mlp_rw.hip ph_*: the exact operations of common.h
     // philox4x32_10 / philox_normal4, every intermediate through a register fence; bit-identical to fetch_noise)
     struct PhSt {
-        uint32_t c0, c1, c2, c3, k0, k1, h;
+        uint32_t c0, c1, c2, c3, k0, k1, h, l;
         float u0, u1, u2, u3, ra, rb;
         float z[4];
     };
@@ -489,14 +489,25 @@ struct MlpH2 {
         auto ff = [](float &x) { asm volatile("" : "+v"(x)); };
         constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
         if (k < 40) {
+            // one round per four micro-steps; each 32 x 32 -> 64-bit product is one v_mad_u64_u32 (both halves of
+            // M x c at the cost of one quarter-rate multiply, instead of a v_mul_hi_u32 and a v_mul_lo_u32)
             switch (k & 3) {
-            case 0: st.h = __umulhi(M0, st.c0); fu(st.h); break;
-            case 1: st.c0 = M0 * st.c0; fu(st.c0); break;
-            case 2: { const uint32_t hi1 = __umulhi(M1, st.c2); st.c3 = st.h ^ st.c3 ^ st.k1; st.h = hi1; fu(st.h); fu(st.c3); } break;
+            case 0: {
+                const uint64_t p0 = (uint64_t)M0 * st.c0;
+                st.h = (uint32_t)(p0 >> 32);
+                st.c0 = (uint32_t)p0;  // lo0 until the round's end
+                fu(st.h); fu(st.c0);
+            } break;
+            case 1: st.c3 = st.h ^ st.c3 ^ st.k1; fu(st.c3); break;  // the round's new c2
+            case 2: {
+                const uint64_t p1 = (uint64_t)M1 * st.c2;
+                st.h = (uint32_t)(p1 >> 32);
+                st.l = (uint32_t)p1;
+                fu(st.h); fu(st.l);
+            } break;
             default: {
-                const uint32_t lo1 = M1 * st.c2;
                 const uint32_t n0 = st.h ^ st.c1 ^ st.k0, n2 = st.c3, n3 = st.c0;
-                st.c0 = n0; st.c1 = lo1; st.c2 = n2; st.c3 = n3;
+                st.c0 = n0; st.c1 = st.l; st.c2 = n2; st.c3 = n3;
                 st.k0 += W0; st.k1 += W1;
                 fu(st.c0); fu(st.c1); fu(st.c2); fu(st.c3);
             } break;
