@@ -373,18 +373,22 @@ struct MlpH2 {
             const int nt = (NT % 4 == 0 || wave + 4 * j < NT) ? wave + 4 * j : 0;
             acc[j][0] = acc[j][1] = *reinterpret_cast<const f32x4 *>(bias + nt * 16 + 4 * q);
         }
+        // both column tiles' operand reads in flight before the first MFMA: one read latency instead of two in a row
+        u32x4 xf[NCT][2];
 #pragma unroll
         for (int c = 0; c < NCT; ++c) {
             const char *b = lds + L::T1 + (c * 16 + col) * L::RS + 16 * (q ^ L::swz(col));
-            u32x4 x[2];
-            x[0] = *reinterpret_cast<const u32x4 *>(b);
-            x[1] = *reinterpret_cast<const u32x4 *>(b + L::PL);
+            xf[c][0] = *reinterpret_cast<const u32x4 *>(b);
+            xf[c][1] = *reinterpret_cast<const u32x4 *>(b + L::PL);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 0; c < NCT; ++c)
 #pragma unroll
             for (int j = 0; j < T; ++j)
                 if (NT % 4 == 0 || wave + 4 * j < NT)
 #pragma unroll
-                    for (int m = 0; m < 3; ++m) acc[j][c] = mfma_h(f.v[j][0][wpl(m)], x[xpl(m)], acc[j][c]);
-        }
+                    for (int m = 0; m < 3; ++m) acc[j][c] = mfma_h(f.v[j][0][wpl(m)], xf[c][xpl(m)], acc[j][c]);
 #pragma unroll
         for (int j = 0; j < T; ++j)
 #pragma unroll
