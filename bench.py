@@ -1,16 +1,17 @@
 """Headline benchmark: candidate trajectories denoised + cost-ranked per second.
 
 BASELINE.json metric "candidate trajectories/sec (100 denoise steps, H=32)". The default workload is
-configs[1] (cfg2): 2D double integrator, 4096 candidates per GPU, H=32, 100 CFG-DDPM steps, MLP
-noise-net (build-defined CFG MLP), fp32-class GEMMs (two-term fp16, csrc/mlp_h2.hip; --dtype f32x3 for
-the six-product split-bf16 kernels). One step = one mpc_step,
-i.e. one mpcd_mpc_step call: context upload, Philox x_T + the denoising loop (2 net evaluations per
-step) + clip flag + fp64 rollout/cost + argmin + winner row (+ RCCL cost all-gather and winner
-exchange for N > 1) + one D2H copy of the applied trajectory. Weak scaling: every rank adds its
-4096 candidates; a multi-rank run also times the strong split (4096 over the ranks) and reports it beside
-the value as "strong_scaling".
+configs[1] (cfg2): 2D double integrator, 4096 candidates, H=32, 100 CFG-DDPM steps, MLP noise-net
+(build-defined CFG MLP), fp32-accurate GEMMs (`f32x3`: every fp32 operand as three bf16 terms,
+six partial products accumulated in fp32, csrc/mlp_rw.hip). `--dtype f16x2` selects the two-term fp16 kernel
+(22 significant bits per operand, fp16 range: NOT fp32 arithmetic, and its line says "dtype": "f16x2"). One step
+= one mpc_step, i.e. one mpcd_mpc_step call: context upload, Philox x_T + the denoising loop (2 net evaluations
+per step) + clip flag + fp64 rollout/cost + argmin + winner row (+ RCCL cost all-gather and winner exchange for
+N > 1) + the applied trajectory to the host. Strong scaling: the workload's B candidates are split
+over the ranks; a multi-rank run also times the weak form (B per rank) and reports it beside the value as
+"weak_scaling".
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg1..cfg5] [--dtype ...]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg1..cfg5|panda] [--dtype ...]
   torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 `--gpus N` without torchrun starts the N rank processes itself (launch_ranks); under torchrun --gpus must
@@ -18,8 +19,8 @@ equal WORLD_SIZE. `--exchange gloo` rehearses the multi-rank bench with every ra
 
 The other BASELINE configs are selectable with --workload (their lines are kept under profiles/):
 cfg1 (the reference's CPU-sized case), cfg3 (pendulum, 1D U-Net, CFG-DDIM 100 steps), cfg4 (cart-pole
-NMPC dynamics, U-Net, H=64, two-term fp16 fused program; 65536 candidates split over the ranks = strong scaling), cfg5 (12-DoF
-quadrotor, U-Net fp16 operands, 250 steps; 131072 candidates split over the ranks).
+NMPC dynamics, U-Net, H=64, fused split-bf16 program), cfg5 (12-DoF quadrotor, U-Net fp16 operands, 250 steps:
+the config BASELINE names "fp16 hidden").
 """
 import argparse
 import json
@@ -39,23 +40,24 @@ sys.path.insert(0, ROOT)
 # the time MLP and cond projections run once per step / per context in the prologues).
 WORKLOADS = {
     "cfg1": dict(workload="cfg1: 2D double integrator, MLP noise-net, CFG-DDPM (reference CPU-sized case)",
-                 system="double_int2d", net="mlp", d=2, H=16, C=4, N=50, B=64, split=False, sampler="ddpm_cfg",
-                 ddim_steps=None, schedule="exponential", dtype="f16x2", mac=117504, mac_row=93184),
+                 system="double_int2d", net="mlp", d=2, H=16, C=4, N=50, B=64, sampler="ddpm_cfg",
+                 ddim_steps=None, schedule="exponential", dtype="f32x3", mac=117504, mac_row=93184),
     "cfg2": dict(workload="cfg2: 2D double integrator, MLP noise-net, CFG-DDPM", system="double_int2d", net="mlp",
-                 d=2, H=32, C=4, N=100, B=4096, split=False, sampler="ddpm_cfg", ddim_steps=None,
-                 schedule="exponential", dtype="f16x2", mac=119552, mac_row=95232),
+                 d=2, H=32, C=4, N=100, B=4096, sampler="ddpm_cfg", ddim_steps=None,
+                 schedule="exponential", dtype="f32x3", mac=119552, mac_row=95232),
     "cfg3": dict(workload="cfg3: pendulum swing-up, 1D temporal U-Net, CFG-DDIM (100 sampling steps)",
-                 system="pendulum", net="unet", d=1, H=32, C=2, N=100, B=16384, split=False, sampler="ddim_cfg",
+                 system="pendulum", net="unet", d=1, H=32, C=2, N=100, B=16384, sampler="ddim_cfg",
                  ddim_steps=100, schedule="exponential", dtype="f32x3", mac=9122560 + 896 * (2 - 5), mac_row=None),
     "cfg4": dict(workload="cfg4: cart-pole (nonlinear NMPC dynamics), 1D temporal U-Net, CFG-DDPM, H=64",
-                 system="cartpole_nl5", net="unet", d=1, H=64, C=5, N=100, B=65536, split=True, sampler="ddpm_cfg",
-                 ddim_steps=None, schedule="exponential", dtype="f16x2", mac=18209152, mac_row=None),
+                 system="cartpole_nl5", net="unet", d=1, H=64, C=5, N=100, B=65536, sampler="ddpm_cfg",
+                 ddim_steps=None, schedule="exponential", dtype="f32x3", mac=18209152, mac_row=None),
     "cfg5": dict(workload="cfg5: 12-DoF quadrotor, 1D temporal U-Net with fp16 GEMM operands, CFG-DDPM 250 steps",
-                 system="quadrotor12", net="unet", d=4, H=64, C=12, N=250, B=131072, split=True, sampler="ddpm_cfg",
+                 system="quadrotor12", net="unet", d=4, H=64, C=12, N=250, B=131072, sampler="ddpm_cfg",
                  ddim_steps=None, schedule="cosine", dtype="f16", mac=18258432, mac_row=None),
 }
 PEAK_FP32 = 157.3e12      # MI355X dense fp32 MFMA / vector peak, FLOP/s (MI355X_MICROARCH.md)
 PEAK_BF16 = 2516.6e12     # MI355X dense bf16 / fp16 MFMA peak: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz
+LIB = os.path.join(ROOT, "mpc_via_diffusion_model_amd", "libmpcd.so")
 PMC_FILES = {("cfg2", "f32"): os.path.join(ROOT, "profiles", "r1_pmc_mlp_sampler.json"),
              ("cfg2", "f32x3"): os.path.join(ROOT, "profiles", "r4_pmc_mlp_rw.json"),
              ("cfg2", "f16x2"): os.path.join(ROOT, "profiles", "r5_pmc_mlp_h2.json"),
@@ -65,6 +67,18 @@ PMC_FILES = {("cfg2", "f32"): os.path.join(ROOT, "profiles", "r1_pmc_mlp_sampler
              ("cfg4", "f32x3"): os.path.join(ROOT, "profiles", "r4_unet_roofline_cfg4.json"),
              ("cfg4", "f16x2"): os.path.join(ROOT, "profiles", "r5_unet_roofline_cfg4_h2.json"),
              ("cfg5", "f16"): os.path.join(ROOT, "profiles", "r3_unet_roofline_cfg5.json")}
+
+
+def lib_sha256(path=None):
+    """sha256 of the loaded product library (MPCD_LIB overrides it, as in _native.py): ties a PMC traffic file to
+    the build it was measured on"""
+    import hashlib
+    path = path or os.environ.get("MPCD_LIB") or LIB
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
 
 
 def _rank_env():
@@ -181,7 +195,7 @@ def panda(args):
 
     from mpc_via_diffusion_model_amd import DiffusionMPC, NetSpec
     torch.cuda.set_device(0)
-    dtype = args.dtype or "f16x2"
+    dtype = args.dtype or "f32x3"
     sd = load_file(PANDA_CKPT)
     plan = DiffusionMPC.from_state_dict(sd, NetSpec("unet", state_dim=7, horizon=128, context_dim=20, dtype=dtype))
     rng = np.random.default_rng(1)
@@ -197,7 +211,8 @@ def panda(args):
 
     out = {"metric": "Panda control-step latency (run_CFG, B=1, H=128, 25 + 5 CFG-DDPM steps, return_chain)",
            "unit": "s", "higher_is_better": False, "n_gpus": 1, "steps": steps, "warmup": warmup,
-           "dtype": "f16" if dtype == "f16" else "f32", "data": "trained panda_test6_117600 EMA weights "
+           "dtype": {"f32": "f32", "f32x3": "f32", "f16x2": "f16x2", "f16": "f16"}[dtype], "numerics": dtype,
+           "data": "trained panda_test6_117600 EMA weights "
            "(tests/golden), synthetic states ~ U[-1,1]^20", "vs_baseline": None,
            "reference_published_s": {"median": PANDA_REF_S, "note": "BASELINE.md / SURVEY §6, unspecified CUDA GPU "
                                      "(eager PyTorch); context only, different hardware"}}
@@ -288,11 +303,10 @@ def main():
                          "rehearsal of the multi-rank bench)")
     ap.add_argument("--steps", type=int, default=None, help="timed control steps (default 50; U-Net configs 5)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed control steps (default 20: the shader clock settles over the first dozen launches; U-Net configs 2, the first one runs the tiling autotune)")
-    ap.add_argument("--scaling", default=None, choices=["strong", "weak"],
-                    help="weak: every GPU runs the workload's B candidates and the units all ranks process add up "
-                         "(a multi-rank run also times the strong split beside it); strong: B_total split over the "
-                         "ranks (SURVEY §8d). Default: strong for the configs BASELINE names as sharded across 8 "
-                         "GPUs (cfg4, cfg5), weak otherwise")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong (default, SURVEY §8d): the workload's B_total candidates split over the ranks (a "
+                         "multi-rank run also times the weak form beside it); weak: every GPU runs B candidates and "
+                         "the units all ranks process add up")
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS) + ["panda"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-shard-probe", action="store_true", help="skip the strong-scaling shard probes (kernel traces)")
@@ -300,8 +314,8 @@ def main():
     ap.add_argument("--candidates", type=int, default=None,
                     help="override the workload's B (profiling a shard size; the line then names the changed config)")
     ap.add_argument("--dtype", default=None, choices=["f32", "f32x3", "f16", "f16x2"],
-                    help="GEMM numerics: exact fp32 MFMA, fp32-accurate split-bf16 MFMA, fp16 operands (U-Net), "
-                         "fp32-class two-term fp16 MFMA (MLP)")
+                    help="GEMM numerics: exact fp32 MFMA, fp32-accurate split-bf16 MFMA (default but cfg5), fp16 "
+                         "operands (cfg5), two-term fp16 MFMA (22-bit operands, fp16 range: labelled f16x2)")
     args = ap.parse_args()
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None:
@@ -340,7 +354,7 @@ def main():
         torch.cuda.set_device(0)
     if cfg["B"] % world:
         raise SystemExit(f"{args.workload}: {cfg['B']} candidates do not split over {world} ranks")
-    if (args.scaling or ("strong" if cfg["split"] else "weak")) == "strong":
+    if args.scaling == "strong":
         b_local, scaling = cfg["B"] // world, "strong"
     else:
         b_local, scaling = cfg["B"], "weak"
@@ -388,13 +402,15 @@ def main():
         return el, float(np.mean(kernel_ms)), res
 
     elapsed, kms, r = timed(b_local)
-    # a weak-scaling multi-rank run also times the strong split (the workload's B over the ranks) in the same job
-    strong = None
-    if world > 1 and scaling == "weak":
-        el_s, kms_s, r_s = timed(cfg["B"] // world)
-        strong = {"candidates_total": cfg["B"], "candidates_per_gpu": cfg["B"] // world, "steps": steps,
-                  "value": cfg["B"] * steps / el_s, "ms_per_step": 1e3 * el_s / steps, "kernel_ms": kms_s,
-                  "best_cost_last_step": r_s.best_cost}
+    # a multi-rank run also times the other form in the same job: weak beside a strong value (B per rank, the
+    # units of all ranks added), strong beside a weak one (the workload's B over the ranks)
+    other = None
+    if world > 1:
+        b_o = cfg["B"] if scaling == "strong" else cfg["B"] // world
+        el_o, kms_o, r_o = timed(b_o)
+        other = {"candidates_total": b_o * world, "candidates_per_gpu": b_o, "steps": steps,
+                 "value": b_o * world * steps / el_o, "ms_per_step": 1e3 * el_o / steps, "kernel_ms": kms_o,
+                 "best_cost_last_step": r_o.best_cost}
 
     # strong scaling: the shard each of P = 2, 4, 8 GPUs gets (B_total / P candidates), measured here on one GPU;
     # (ms_per_step at B_total) / (ms_per_step at B_total / P) is the compute-only P-GPU speedup bound
@@ -472,20 +488,27 @@ def main():
         else:
             roof = {"bound": "mfma", "achieved": achieved / 1e12, "peak": PEAK_FP32 / 1e12, "unit": "TFLOP/s",
                     "frac": achieved / PEAK_FP32, "kernel": kname, "flop_per_launch": flops_launch}
-        traffic = None
+        # traffic: HBM bytes per launch from a PMC pass of this workload (FETCH_SIZE x 2 + WRITE_SIZE, tools/
+        # pmc_summary.py); the file records the sha256 of the library it was measured on, and the line says whether
+        # that is the library this run loaded
+        traffic, traffic_source = None, None
         pmc = PMC_FILES.get((args.workload, dtype))
         if pmc and os.path.exists(pmc):
             with open(pmc) as f:
                 pm = json.load(f)
             if "hbm_bytes_per_forward" in pm:  # one sample call = n_evals forwards; bytes scale with the rows
                 traffic = pm["hbm_bytes_per_forward"] * n_evals * b_local / pm["B"]
-            else:
+            elif pm.get("B", b_local) == b_local or "B" not in pm:
                 traffic = pm.get("hbm_bytes_per_launch")
+            same = pm.get("lib_sha256") is not None and pm.get("lib_sha256") == lib_sha256()
+            traffic_source = {"file": os.path.relpath(pmc, ROOT), "same_build": same,
+                              "kind": "PMC pass of this workload on the library this run loaded" if same else
+                                      "static: PMC pass of this workload on an earlier build (not re-measured)"}
         gemm = {"f32": "exact fp32 MFMA (v_mfma_f32_16x16x4_f32)",
                 "f32x3": "fp32-accurate split-bf16 MFMA (3 bf16 terms per operand, 6 partial products, fp32 accumulate)",
-                "f16x2": "fp32-class two-term fp16 MFMA (hi + lo fp16 per operand, weights scaled per layer by a power of "
-                         "two; 3 partial products, fp32 accumulate): the MLP's CFG-DDPM kernel / the fused U-Net; the "
-                         "f32x3 kernels otherwise",
+                "f16x2": "two-term fp16 MFMA (hi + lo fp16 per operand: 22 significant bits, the fp16 range; weights "
+                         "scaled per layer by a power of two; 3 partial products, fp32 accumulate): NOT fp32 "
+                         "arithmetic; the MLP's CFG-DDPM kernel / the fused U-Net, the f32x3 kernels otherwise",
                 "f16": "fp16 operands, fp32 accumulate (v_mfma_f32_16x16x32_f16)"}[dtype]
         out = {
             "metric": "candidate trajectories/sec (100 denoise steps, H=32)" if args.workload == "cfg2" else
@@ -499,7 +522,10 @@ def main():
             "higher_is_better": True,
             "scaling": scaling,
             "vs_baseline": None,
-            "dtype": "f16" if dtype == "f16" else "f32",  # f16x2 / f32x3: fp32-class results (tests/test_gpu_headline.py)
+            # the arithmetic the GEMMs run: f32x3 reproduces fp32 (three bf16 terms per operand, 24 significant bits,
+            # fp32 range, fp32 accumulation); f16x2 (22 bits, fp16 range) and f16 say so
+            "dtype": {"f32": "f32", "f32x3": "f32", "f16x2": "f16x2", "f16": "f16"}[dtype],
+            "numerics": dtype,
             "data": f"synthetic (random-init weights seed 0 by PyTorch's default-init rule, x0 ~ U[-1,1]^{cfg['C']}, "
                     "Philox noise)",
             "config": {"workload": cfg["workload"], "candidates_per_gpu": b_local, "candidates_total": b_local * world,
@@ -510,12 +536,16 @@ def main():
                                     "(rehearsal)" if gloo else "RCCL inside libmpcd.so (cost all-gather + winner "
                                     "all-reduce), one GPU per rank"),
                        "gemm": gemm},
-            "roofline": dict(roof, traffic=traffic, kernel_ms=kms, timed=timed_desc),
+            "roofline": dict(roof, traffic=traffic, traffic_source=traffic_source, kernel_ms=kms, timed=timed_desc),
             "best_cost_last_step": r.best_cost,
         }
-        if strong is not None:
-            out["strong_scaling"] = dict(strong, note="the same job's strong split: the workload's B candidates "
-                                                      "over the ranks, timed like value (max over ranks)")
+        if other is not None:
+            if scaling == "strong":
+                out["weak_scaling"] = dict(other, note="the same job's weak form: B candidates per rank, the units "
+                                                       "of all ranks added, timed like value (max over ranks)")
+            else:
+                out["strong_scaling"] = dict(other, note="the same job's strong split: the workload's B candidates "
+                                                         "over the ranks, timed like value (max over ranks)")
         if shard_probe:
             out["strong_shard_probe"] = {
                 "note": "one GPU running the B_total/P-candidate shard each of P GPUs gets under strong scaling "

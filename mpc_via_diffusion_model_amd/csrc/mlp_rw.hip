@@ -112,6 +112,16 @@ struct MlpRw {
     static constexpr int CPW = L::CPW;
     static constexpr int QUADS = D0 / 4;
 
+    // Row swizzle of every activation plane (as mlp_h2.hip's Lds2): in rows with bit 2 set the 16-byte units are
+    // swapped in pairs (byte offset b -> b ^ 16). The B-fragment reads (ds_read_b128 of whole units, lane (col, q)
+    // reading unit q ^ s of its row) stay conflict-free; the epilogue's ds_write_b64 of 16 rows at one feature
+    // offset (one lane group, banks mod 32) drop from 4-way to 2-way bank conflicts - 2-way is that pattern's
+    // floor (16 rows on the 8 unit positions of 128 bytes). s = bit 2 of the row = bit 2 of the lane's column in
+    // every layout here (rows ct * 16 + col, or the candidate col / col & 7 of the shared layer-0 input).
+    static MPCD_DEV int swz(int r) { return (r >> 2) & 1; }
+    // byte offset in its row of the 4 features n..n+3 (n = 16 nt + 4 q) an epilogue lane of quarter q stores
+    static MPCD_DEV int st_off(int n, int q, int row) { return n * 2 - 8 * q + 8 * (q ^ (swz(row) << 1)); }
+
     // R = 16 with CFG: columns 0-7 are the context rows of candidates 0-7, 8-15 their masked rows
     static MPCD_DEV int cand_of(int ct, int col) { return NB == 2 ? (R == 16 ? (col & 7) : col) : ct * 16 + col; }
     static MPCD_DEV bool masked_of(int ct, int col) { return NB == 2 && (R == 16 ? col >= 8 : ct == 1); }
@@ -247,7 +257,7 @@ struct MlpRw {
             for (int c = 0; c < NC; ++c) {
                 const int ct = ct_of<l>(wave, c);
                 const int row = in_shared ? cand_of(ct, col) : ct * 16 + col;
-                load_x3(x[c], lds + L::in_off(l) + row * L::in_rs(l) + (kc * 32 + 8 * q) * 2, L::in_pl(l));
+                load_x3(x[c], lds + L::in_off(l) + row * L::in_rs(l) + kc * 64 + 16 * (q ^ swz(row)), L::in_pl(l));
             }
         };
         auto epi = [&](int j, int c) {
@@ -261,7 +271,8 @@ struct MlpRw {
             }
             u32x2 p0, p1, p2;
             split3(v, p0, p1, p2);
-            char *o = lds + L::out_off(l) + (ct_of<l>(wave, c) * 16 + col) * L::out_rs(l) + n * 2;
+            const int ro = ct_of<l>(wave, c) * 16 + col;
+            char *o = lds + L::out_off(l) + ro * L::out_rs(l) + st_off(n, q, ro);
             *reinterpret_cast<u32x2 *>(o) = p0;
             *reinterpret_cast<u32x2 *>(o + L::out_pl(l)) = p1;
             *reinterpret_cast<u32x2 *>(o + 2 * L::out_pl(l)) = p2;
@@ -326,7 +337,7 @@ struct MlpRw {
         auto ldx = [&](u32x4 (&x)[3], int i) {  // step i = (pass i / KC, k-chunk i % KC)
             const int p = i / KC, kc = i % KC, ct = ct_of<l>(wave, cp(p));
             const int row = in_shared ? cand_of(ct, col) : ct * 16 + col;
-            load_x3(x, lds + L::in_off(l) + row * L::in_rs(l) + (kc * 32 + 8 * q) * 2, L::in_pl(l));
+            load_x3(x, lds + L::in_off(l) + row * L::in_rs(l) + kc * 64 + 16 * (q ^ swz(row)), L::in_pl(l));
         };
         // epilogue of pass p in five units: Mish of element 0..3, then the split + the three plane stores
         auto epi_unit = [&](int u, f32x4 &v, int p) {
@@ -337,7 +348,8 @@ struct MlpRw {
             const int n = nt_of<l>(wave, jp(p)) * 16 + 4 * q;
             u32x2 p0, p1, p2;
             split3(v, p0, p1, p2);
-            char *o = lds + L::out_off(l) + (ct_of<l>(wave, cp(p)) * 16 + col) * L::out_rs(l) + n * 2;
+            const int ro = ct_of<l>(wave, cp(p)) * 16 + col;
+            char *o = lds + L::out_off(l) + ro * L::out_rs(l) + st_off(n, q, ro);
             *reinterpret_cast<u32x2 *>(o) = p0;
             *reinterpret_cast<u32x2 *>(o + L::out_pl(l)) = p1;
             *reinterpret_cast<u32x2 *>(o + 2 * L::out_pl(l)) = p2;
@@ -369,7 +381,8 @@ struct MlpRw {
             }
             const int s = EPI != EPI_NONE ? k - 16 : k;
             const int n = nt_of<l>(wave, jp(p)) * 16 + 4 * q;
-            char *o = lds + L::out_off(l) + (ct_of<l>(wave, cp(p)) * 16 + col) * L::out_rs(l) + n * 2;
+            const int ro = ct_of<l>(wave, cp(p)) * 16 + col;
+            char *o = lds + L::out_off(l) + ro * L::out_rs(l) + st_off(n, q, ro);
             switch (s) {  // split3 (mlp_x3.h), in pieces
             case 0: ep0 = u32x2{pk_bf16(ev.x, ev.y), pk_bf16(ev.z, ev.w)}; break;
             case 1: er.x = ev.x - bf_lo(ep0.x); er.y = ev.y - bf_hi(ep0.x); break;
@@ -489,7 +502,7 @@ struct MlpRw {
         *reinterpret_cast<f32x4 *>(lds + L::XB + (cl * L::SX + n) * 4) = x;
         u32x2 p0, p1, p2;
         split3(x, p0, p1, p2);
-        char *o = lds + L::S1 + cl * L::RS + n * 2;
+        char *o = lds + L::S1 + cl * L::RS + ((n * 2) ^ (swz(cl) << 4));
         *reinterpret_cast<u32x2 *>(o) = p0;
         *reinterpret_cast<u32x2 *>(o + L::PL) = p1;
         *reinterpret_cast<u32x2 *>(o + 2 * L::PL) = p2;
@@ -530,14 +543,16 @@ struct MlpRw {
             const int nt = (NT % 4 == 0 || wave + 4 * j < NT) ? wave + 4 * j : 0;
             acc[j][0] = acc[j][1] = *reinterpret_cast<const f32x4 *>(bias + nt * 16 + 4 * q);
         }
+        // both column tiles' operand reads in flight before the first MFMA: one LDS latency instead of two in a row
+        u32x4 xf[NCT][3];
 #pragma unroll
-        for (int c = 0; c < NCT; ++c) {
-            u32x4 x[3];
-            load_x3(x, lds + L::T1 + (c * 16 + col) * L::RS + 8 * q * 2, L::PL);
+        for (int c = 0; c < NCT; ++c) load_x3(xf[c], lds + L::T1 + (c * 16 + col) * L::RS + 16 * (q ^ swz(col)), L::PL);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 0; c < NCT; ++c)
 #pragma unroll
             for (int j = 0; j < T; ++j)
-                if (NT % 4 == 0 || wave + 4 * j < NT) acc[j][c] = mfma_x3(f.v[j][0], x, acc[j][c]);
-        }
+                if (NT % 4 == 0 || wave + 4 * j < NT) acc[j][c] = mfma_x3(f.v[j][0], xf[c], acc[j][c]);
         MPCD_FINAL_MARK(28, acc[0][1]);  // experiment build: the final layer's operand reads and MFMAs
 #ifdef MPCD_PROF_FINAL_MFMA_ONLY
         // timing experiment (wrong results): the final layer's MFMAs only, no update

@@ -50,19 +50,24 @@ def _line(r):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(400)
-def test_bench_two_ranks_on_one_gpu_strong():
-    out = _line(_run(["--gpus", "2", "--exchange", "gloo", "--scaling", "strong", "--steps", "3", "--warmup", "1",
-                      "--no-cpu-baseline"]))
+def test_bench_two_ranks_on_one_gpu_default_is_strong():
+    """The default multi-rank line is SURVEY §8d's strong scaling: cfg2's 4,096 candidates split over the ranks,
+    value = 4,096 x steps / time; the weak form (4,096 per rank) is reported beside it."""
+    out = _line(_run(["--gpus", "2", "--exchange", "gloo", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]))
     assert out["n_gpus"] == 2 and out["scaling"] == "strong"
     assert out["config"]["candidates_total"] == 4096 and out["config"]["candidates_per_gpu"] == 2048
     assert out["config"]["parallelism"] == "dp2" and "gloo" in out["config"]["exchange"]
     assert out["value"] > 0 and out["steps"] == 3 and out["cpu_baseline"] is None
+    assert out["dtype"] == "f32" and out["numerics"] == "f32x3"
+    wk = out["weak_scaling"]
+    assert wk["candidates_total"] == 8192 and wk["candidates_per_gpu"] == 4096 and wk["value"] > 0
 
 
 @pytest.mark.gpu
 @pytest.mark.timeout(400)
 def test_bench_two_ranks_on_one_gpu_weak_reports_the_strong_split():
-    out = _line(_run(["--gpus", "2", "--exchange", "gloo", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]))
+    out = _line(_run(["--gpus", "2", "--exchange", "gloo", "--scaling", "weak", "--steps", "3", "--warmup", "1",
+                      "--no-cpu-baseline"]))
     assert out["n_gpus"] == 2 and out["scaling"] == "weak"
     assert out["config"]["candidates_total"] == 8192 and out["config"]["candidates_per_gpu"] == 4096
     st = out["strong_scaling"]

@@ -52,6 +52,8 @@ run_job() {
         python3 bench.py --workload "$w" --no-cpu-baseline --no-shard-probe $BENCH_ARGS > "gpurun_out/prof/trace_$w.log" 2>&1 ;;
     pmc)
       local w=${arg:-cfg2} c
+      # the library the passes measure (tools/pmc_summary.py records it; bench.py compares it with the one it loads)
+      sha256sum mpc_via_diffusion_model_amd/libmpcd.so | cut -d' ' -f1 > "gpurun_out/prof/pmc_${w}_lib.sha256"
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 300 rocprofv3 --pmc $c -d "gpurun_out/prof/pmc_${w}_$c" -o run -f csv -- \
           python3 bench.py --workload "$w" --no-cpu-baseline --steps 3 --warmup 1 $BENCH_ARGS \

@@ -7,6 +7,7 @@ half the bytes of 16-B/lane streaming reads; WRITE_SIZE is exact for 16-B stores
 process is cold (weights not yet in the Infinity Cache / L2) and is reported separately."""
 import csv
 import json
+import os
 import sys
 
 
@@ -31,6 +32,11 @@ def main(fetch_dir, write_dir, label, out, only=None):
            "hbm_bytes_note": "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 averaged over the warm launches (2..n)"}
     if only:
         res["kernel_filter"] = only
+    # sha256 of the library the passes ran on (tools/gpu.sh pmc writes it beside the pass directories)
+    sha = os.path.join(os.path.dirname(os.path.abspath(fetch_dir)),
+                       os.path.basename(fetch_dir.rstrip("/")).rsplit("_", 1)[0] + "_lib.sha256")
+    if os.path.exists(sha):
+        res["lib_sha256"] = open(sha).read().split()[0]
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
