@@ -56,12 +56,14 @@ enum mpcd_net_kind {
  *             partial products >= 2^-16 of the leading one accumulated in fp32 (error at the level of
  *             the fp32 MFMA's). MLP: needs a context shared by all candidates (or none); a
  *             per-candidate context runs the MPCD_F32 kernel.
- * MPCD_F16X2: fp32-class two-term fp16 MFMA (MLP only, csrc/mlp_h2.hip): each fp32 operand = hi + lo (two fp16,
- *             the weights scaled per layer by an exact power of two), three products per 32-k chunk accumulated
- *             in fp32 (error <= 2^-22 of |w||x| per product, the order of fp32's own summation error). Used for
- *             the CFG-DDPM sampler and the eps forward at H*d = 32 / 64 with a shared context; every other case
- *             (unclamped DDIM, whose unbounded x leaves the fp16 range; per-candidate contexts; H*d = 128) runs
- *             the MPCD_F32X3 kernels of the same net. */
+ * MPCD_F16X2: two-term fp16 MFMA (MLP: csrc/mlp_h2.hip; U-Net: the fused P = 2 program) - NOT fp32 arithmetic:
+ *             each operand = hi + lo (two fp16, the weights scaled per layer by an exact power of two, the
+ *             activations unscaled), three products per 32-k chunk accumulated in fp32. 22 significant bits per
+ *             operand (fp32: 24) and the fp16 range: an activation above 65504 becomes a NaN sample (mpcd_mpc_step
+ *             then re-runs the step in MPCD_F32X3, see mpcd_force_f32x3), activations below 2^-14 keep an
+ *             absolute, not relative, precision of 2^-25. Used for the CFG-DDPM sampler and the eps forward (MLP at
+ *             H*d = 32 / 64 with a shared context); every other case (unclamped DDIM, whose unbounded x leaves
+ *             the fp16 range; per-candidate contexts; H*d = 128) runs the MPCD_F32X3 kernels of the same net. */
 enum mpcd_dtype { MPCD_F32 = 0, MPCD_F16 = 1, MPCD_F32X3 = 2, MPCD_F16X2 = 3 };
 
 typedef struct {
@@ -332,8 +334,10 @@ int mpcd_mpc_step(mpcd_ctx *ctx, const mpcd_step_args *args, mpcd_best *best_hos
  * bit 0 (MPCD_STEP_CLIPPED): LimitsNormalizer's global clip was applied; bit 1 (MPCD_STEP_NAN_SAMPLES): some
  * candidate's tested tensor (its chain under MPCD_CLIP_CHAIN, its final sample under MPCD_CLIP_FINAL) holds a
  * NaN on some rank - the reference's torch max()/min() are then NaN and nothing is clipped; bit 2
- * (MPCD_STEP_NONFINITE_WINNER): no finite cost (the call returned MPCD_ENONFINITE). */
-enum { MPCD_STEP_CLIPPED = 1, MPCD_STEP_NAN_SAMPLES = 2, MPCD_STEP_NONFINITE_WINNER = 4 };
+ * (MPCD_STEP_NONFINITE_WINNER): no finite cost (the call returned MPCD_ENONFINITE); bit 3 (MPCD_STEP_F32X3_RERUN): an
+ * MPCD_F16X2 net's step left the fp16 range (NaN samples or no finite cost, one rank) and was re-run with the net's
+ * split-bf16 programs - the other bits and the outputs are the re-run's. */
+enum { MPCD_STEP_CLIPPED = 1, MPCD_STEP_NAN_SAMPLES = 2, MPCD_STEP_NONFINITE_WINNER = 4, MPCD_STEP_F32X3_RERUN = 8 };
 int mpcd_last_step_flags(mpcd_ctx *ctx, int32_t *flags);
 
 /* U-Net conv tilings (MPCD_F32X3 / MPCD_F16). Each conv launch picks rows-per-workgroup x register tile
@@ -359,6 +363,10 @@ int mpcd_mlp_layout(int64_t batch, int32_t cfg_masked, int32_t *layout_out);
  * mlp_rw_kernel), 2 two-term fp16 (mlp_h2_kernel); out[1] = the bf16x3 layout (as mpcd_mlp_layout) or -1;
  * out[2] = rows per workgroup (32 or 16). MPCD_EUNSUP on a U-Net context. */
 int mpcd_mlp_form(mpcd_ctx *ctx, int32_t sampler, int64_t batch, int32_t out[3]);
+/* on != 0: an MPCD_F16X2 net runs its split-bf16 (MPCD_F32X3) programs for every call on this context until turned
+ * off again (mpcd_mpc_step does this by itself for one re-run when an MPCD_F16X2 step's samples come back with a NaN
+ * or without a finite cost: the fp16 range was left; MPCD_STEP_F32X3_RERUN flags it). */
+int mpcd_force_f32x3(mpcd_ctx *ctx, int32_t on);
 /* U-Net execution form, process-wide. The whole-network form (csrc/unet_fused.hip: every conv of one denoise
  * step in ONE launch, a workgroup per few candidates, activations in LDS) covers the CFG samplers and the
  * two-branch eps of ConditionedTemporalUnet(base 32, dim_mults (1, 2, 4)) at H = 32 / 64 with the MPCD_F32X3

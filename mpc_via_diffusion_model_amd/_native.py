@@ -22,7 +22,7 @@ MPCD_CLIP_CHAIN, MPCD_CLIP_FINAL, MPCD_CLIP_NONE = 0, 1, 2
 
 _STATUS = {-1: "EINVAL", -2: "EHIP", -3: "ESTATE", -4: "ENOMEM", -5: "EUNSUP", -6: "ENONFINITE"}
 MPCD_ENONFINITE = -6
-MPCD_STEP_CLIPPED, MPCD_STEP_NAN_SAMPLES, MPCD_STEP_NONFINITE_WINNER = 1, 2, 4
+MPCD_STEP_CLIPPED, MPCD_STEP_NAN_SAMPLES, MPCD_STEP_NONFINITE_WINNER, MPCD_STEP_F32X3_RERUN = 1, 2, 4, 8
 
 
 class NetDesc(ctypes.Structure):
@@ -105,6 +105,7 @@ EXPORTS = {
     "mpcd_last_step_flags": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "mpcd_unet_force_tiling": ([ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
     "mpcd_mlp_force_layout": ([ctypes.c_int32], ctypes.c_int),
+    "mpcd_force_f32x3": ([ctypes.c_void_p, ctypes.c_int32], ctypes.c_int),
     "mpcd_mlp_layout": ([ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "mpcd_mlp_form": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "mpcd_unet_force_path": ([ctypes.c_int32], ctypes.c_int),

@@ -365,7 +365,7 @@ struct MlpRw {
         // common.h mish() and split3(); every intermediate through an empty register fence (no SLP packing).
         float et[4];
         u32x2 ep0, ep1, ep2;
-        f32x4 er = ev;
+        float er0 = 0.f, er1 = 0.f, er2 = 0.f, er3 = 0.f;
         constexpr int NSTEP = (EPI != EPI_NONE ? 16 : 0) + 8;
         auto fence = [](float &x) { asm volatile("" : "+v"(x)); };
         auto epi_step = [&](int k, int p) {
@@ -384,13 +384,16 @@ struct MlpRw {
             const int ro = ct_of<l>(wave, cp(p)) * 16 + col;
             char *o = lds + L::out_off(l) + ro * L::out_rs(l) + st_off(n, q, ro);
             switch (s) {  // split3 (mlp_x3.h), in pieces
+            // each remainder through a fence: the compiler would otherwise pair the two subtractions of a step
+            // into one v_pk_add_f32, which beside MFMAs costs more issue time than the two plain ones
+            // (MI355X_MICROARCH.md, price of one filler beside MFMAs)
             case 0: ep0 = u32x2{pk_bf16(ev.x, ev.y), pk_bf16(ev.z, ev.w)}; break;
-            case 1: er.x = ev.x - bf_lo(ep0.x); er.y = ev.y - bf_hi(ep0.x); break;
-            case 2: er.z = ev.z - bf_lo(ep0.y); er.w = ev.w - bf_hi(ep0.y); *reinterpret_cast<u32x2 *>(o) = ep0; break;
-            case 3: ep1 = u32x2{pk_bf16(er.x, er.y), pk_bf16(er.z, er.w)}; break;
-            case 4: er.x = er.x - bf_lo(ep1.x); er.y = er.y - bf_hi(ep1.x); break;
-            case 5: er.z = er.z - bf_lo(ep1.y); er.w = er.w - bf_hi(ep1.y); break;
-            case 6: *reinterpret_cast<u32x2 *>(o + L::out_pl(l)) = ep1; ep2 = u32x2{pk_bf16(er.x, er.y), pk_bf16(er.z, er.w)}; break;
+            case 1: er0 = ev.x - bf_lo(ep0.x); fence(er0); er1 = ev.y - bf_hi(ep0.x); fence(er1); break;
+            case 2: er2 = ev.z - bf_lo(ep0.y); fence(er2); er3 = ev.w - bf_hi(ep0.y); fence(er3); *reinterpret_cast<u32x2 *>(o) = ep0; break;
+            case 3: ep1 = u32x2{pk_bf16(er0, er1), pk_bf16(er2, er3)}; break;
+            case 4: er0 = er0 - bf_lo(ep1.x); fence(er0); er1 = er1 - bf_hi(ep1.x); fence(er1); break;
+            case 5: er2 = er2 - bf_lo(ep1.y); fence(er2); er3 = er3 - bf_hi(ep1.y); fence(er3); break;
+            case 6: *reinterpret_cast<u32x2 *>(o + L::out_pl(l)) = ep1; ep2 = u32x2{pk_bf16(er0, er1), pk_bf16(er2, er3)}; break;
             default: *reinterpret_cast<u32x2 *>(o + 2 * L::out_pl(l)) = ep2; break;
             }
         };
@@ -497,11 +500,26 @@ struct MlpRw {
     }
 
     // x (4 features) -> fp32 row in XB and the three bf16 planes layer 0 reads
+    // split3 (mlp_x3.h) with every remainder through a fence: the same values, no v_pk_add_f32
+    static MPCD_DEV void split3s(const f32x4 &v, u32x2 &p0, u32x2 &p1, u32x2 &p2)
+    {
+        auto fence = [](float &x) { asm volatile("" : "+v"(x)); };
+        const uint32_t a = pk_bf16(v.x, v.y), b = pk_bf16(v.z, v.w);
+        float r0 = v.x - bf_lo(a), r1 = v.y - bf_hi(a), r2 = v.z - bf_lo(b), r3 = v.w - bf_hi(b);
+        fence(r0); fence(r1); fence(r2); fence(r3);
+        const uint32_t c = pk_bf16(r0, r1), d = pk_bf16(r2, r3);
+        r0 = r0 - bf_lo(c); r1 = r1 - bf_hi(c); r2 = r2 - bf_lo(d); r3 = r3 - bf_hi(d);
+        fence(r0); fence(r1); fence(r2); fence(r3);
+        p0 = u32x2{a, b};
+        p1 = u32x2{c, d};
+        p2 = u32x2{pk_bf16(r0, r1), pk_bf16(r2, r3)};
+    }
+
     static MPCD_DEV void store_x(char *lds, int cl, int n, const f32x4 &x)
     {
         *reinterpret_cast<f32x4 *>(lds + L::XB + (cl * L::SX + n) * 4) = x;
         u32x2 p0, p1, p2;
-        split3(x, p0, p1, p2);
+        split3s(x, p0, p1, p2);
         char *o = lds + L::S1 + cl * L::RS + ((n * 2) ^ (swz(cl) << 4));
         *reinterpret_cast<u32x2 *>(o) = p0;
         *reinterpret_cast<u32x2 *>(o + L::PL) = p1;

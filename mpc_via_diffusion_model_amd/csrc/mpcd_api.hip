@@ -264,6 +264,7 @@ struct mpcd_ctx {
     DevBuf wpackh;      // MLP linear layers as two fp16 planes + per-layer scales (MPCD_F16X2)
     DevBuf cond_layers; // CondLayer[n_cond]
     UnetWeights unet{}; // device pointers into `params` + repacked conv weights
+    bool force_x3 = false;  // mpcd_force_f32x3: an MPCD_F16X2 net runs its split-bf16 (MPCD_F32X3) programs
     DevBuf unet_pack;
     // schedule
     std::vector<float> tables;  // 12 x N
@@ -482,7 +483,8 @@ enum { MLPK_F32 = 0, MLPK_X3 = 1, MLPK_H2 = 2 };
 int mlp_kernel_of(const mpcd_ctx *c, int mode, bool shared_ctx)
 {
     const int d0 = c->desc.horizon * c->desc.state_dim;
-    if (c->desc.dtype == MPCD_F16X2 && shared_ctx && c->wpackh.p && mlp_h2_supports(d0, mode)) return MLPK_H2;
+    if (c->desc.dtype == MPCD_F16X2 && !c->force_x3 && shared_ctx && c->wpackh.p && mlp_h2_supports(d0, mode))
+        return MLPK_H2;
     if ((c->desc.dtype == MPCD_F32X3 || c->desc.dtype == MPCD_F16X2) && shared_ctx) return MLPK_X3;
     return MLPK_F32;
 }
@@ -866,6 +868,14 @@ int mpcd_mlp_form(mpcd_ctx *c, int32_t sampler, int64_t batch, int32_t out[3])
     return MPCD_OK;
 }
 
+int mpcd_force_f32x3(mpcd_ctx *c, int32_t on)
+{
+    if (!c) return fail(MPCD_EINVAL, "null context");
+    c->force_x3 = on != 0;
+    c->unet.force3 = on != 0;
+    return MPCD_OK;
+}
+
 int mpcd_mlp_layout(int64_t batch, int32_t cfg_masked, int32_t *layout_out)
 {
     if (batch < 1 || !layout_out) return fail(MPCD_EINVAL, "mpcd_mlp_layout: bad arguments");
@@ -1122,7 +1132,26 @@ int mpcd_select(mpcd_ctx *c, const double *cost_local, int64_t n_local, const fl
     return comm_reduce(c, row_out, (size_t)row_len, COMM_SUM_F32, st);
 }
 
+static int mpc_step_impl(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, float *u_best_host, void *stream);
+
+// An MPCD_F16X2 net computes in the fp16 range: a step whose sampled trajectories came back with a NaN (an
+// activation beyond 65504 turns into one: hi = inf, lo = inf - inf) or with no finite cost is re-run with the net's
+// split-bf16 (MPCD_F32X3) programs and flagged MPCD_STEP_F32X3_RERUN. Single rank only: with a communicator every
+// rank would have to agree to re-run (the flag and the ENONFINITE return report it there).
 int mpcd_mpc_step(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, float *u_best_host, void *stream)
+{
+    int rc = mpc_step_impl(c, a, best_host, u_best_host, stream);
+    const bool f16x2 = c && c->net_loaded && c->desc.dtype == MPCD_F16X2 && !c->force_x3;
+    if (f16x2 && !c->comm && (rc == MPCD_ENONFINITE || (rc == MPCD_OK && (c->step_flags & MPCD_STEP_NAN_SAMPLES)))) {
+        c->force_x3 = c->unet.force3 = true;
+        rc = mpc_step_impl(c, a, best_host, u_best_host, stream);
+        c->force_x3 = c->unet.force3 = false;
+        c->step_flags |= MPCD_STEP_F32X3_RERUN;
+    }
+    return rc;
+}
+
+static int mpc_step_impl(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_host, float *u_best_host, void *stream)
 {
     if (!c || !a || !a->sys || !a->x0 || !a->act_min || !a->act_max || !a->cost_local || !best_host || !u_best_host)
         return fail(MPCD_EINVAL, "null argument");

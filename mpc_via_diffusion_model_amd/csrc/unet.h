@@ -85,6 +85,7 @@ struct UnetWeights {
     std::shared_ptr<UnetFusedPlan> fused3; // MPCD_F16X2 nets: the split-bf16 fused program, for the unclamped DDIM
                                            // samplers (their x leaves the fp16 range)
     std::string fused_why;                 // why not (diagnostics)
+    bool force3 = false;                   // mpcd_force_f32x3: an MPCD_F16X2 net runs its split-bf16 program everywhere
 };
 
 struct UnetSampleArgs {

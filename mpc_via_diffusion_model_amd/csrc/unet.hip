@@ -827,7 +827,7 @@ std::atomic<int> g_unet_path{0};  // mpcd_unet_force_path
 // the fused program a sampler mode runs: an MPCD_F16X2 net's unclamped DDIM samplers take its split-bf16 program
 const UnetFusedPlan *fused_plan(const UnetWeights &W, int mode)
 {
-    if (W.fused_planes == 2 && (mode == MODE_DDIM_CFG || mode == MODE_DDIM)) return W.fused3.get();
+    if (W.fused_planes == 2 && (W.force3 || mode == MODE_DDIM_CFG || mode == MODE_DDIM)) return W.fused3.get();
     return W.fused.get();
 }
 

@@ -81,8 +81,9 @@ class NetSpec:
     cfg: bool = True          # 4-arg net with the CFG context mask
     # GEMM numerics (include/mpcd.h mpcd_dtype): "f32" exact fp32 MFMA; "f32x3" fp32-accurate split-bf16
     # MFMA (MLP: shared or no context; UNet: any); "f16" fp16 operands / fp32 accumulate (UNet, cfg 5); "f16x2"
-    # fp32-class two-term fp16 MFMA (MLP: the CFG-DDPM sampler / eps forward at H*d 32 or 64 with a shared context;
-    # the other cases of such a net run its f32x3 kernels)
+    # two-term fp16 MFMA - NOT fp32 arithmetic: 22-bit operands in the fp16 range (MLP: the CFG-DDPM sampler / eps
+    # forward at H*d 32 or 64 with a shared context; U-Net: the fused CFG-DDPM program; the other cases of such a
+    # net run its f32x3 kernels). A call that leaves the fp16 range (NaN in the chain) is re-run in f32x3.
     dtype: str = "f32"
 
     def desc(self):
@@ -303,9 +304,23 @@ class DiffusionMPC:
         if absmax_out is not None and (absmax_out.dtype != torch.float32 or absmax_out.numel() != B
                                        or absmax_out.device != self.device or not absmax_out.is_contiguous()):
             raise ValueError(f"absmax_out must be a contiguous fp32 [{B}] tensor on {self.device}")
+        # f16x2 numerics compute in the fp16 range: ask for the chain maxima (a NaN there = a value left the range),
+        # check them (one synchronisation) and re-run the call with the net's split-bf16 programs if so
+        guard = self.spec.dtype == "f16x2"
+        amax = absmax_out
+        if guard and amax is None:
+            amax = torch.empty(B, dtype=torch.float32, device=self.device)
         a = self._args(sampler, B, context, w, n_wo_noise, ddim_steps, clamp_x0, seed, global_offset, noise, x, chain,
-                       absmax_out)
+                       amax)
         N.check(self._lib.mpcd_sample(self._ctx, ctypes.byref(a), self._stream()), "mpcd_sample")
+        self.last_f32x3_rerun = False
+        if guard and bool(torch.isnan(amax).any()):
+            N.check(self._lib.mpcd_force_f32x3(self._ctx, 1), "mpcd_force_f32x3")
+            try:
+                N.check(self._lib.mpcd_sample(self._ctx, ctypes.byref(a), self._stream()), "mpcd_sample (f32x3 re-run)")
+            finally:
+                N.check(self._lib.mpcd_force_f32x3(self._ctx, 0), "mpcd_force_f32x3")
+            self.last_f32x3_rerun = True
         return chain if return_chain else x
 
     def run_CFG(self, context=None, hard_conds=None, context_weight=0.1, n_samples=1, horizon=8,

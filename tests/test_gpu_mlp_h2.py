@@ -2,8 +2,9 @@
 (tests/test_gpu_mlp.py runs every oracle case with dtype "f16x2" too): the kernel that runs is the h2 kernel where
 it applies and the f32x3 / f32 kernels where it does not; its two workgroup forms (32 and 16 rows) give the same
 bits; full-size agreement with the exact-fp32 kernel; the per-layer weight scales keep tiny and large weights
-exact to the bar; a net whose activations leave the fp16 range gives a non-finite sample, which the chain |x|
-maximum reports (no silent wrong value). Reference net: temporal_unet.py:451-550 / layers.py:358-385 (SURVEY A11,
+to the bar; large and tiny activations meet the bar; a net whose activations leave the fp16 range is re-run with the
+net's split-bf16 kernels (planner and mpcd_mpc_step), never returned as a NaN or a silently wrong value. f16x2 is
+22-bit operands in the fp16 range, NOT fp32 arithmetic (include/mpcd.h). Reference net: temporal_unet.py:451-550 / layers.py:358-385 (SURVEY A11,
 build-defined CFG MLP)."""
 import numpy as np
 import pytest
@@ -73,28 +74,88 @@ def test_full_size_against_exact_f32():
     assert float(rel.max()) < 1e-4 and float(el) < 1e-4
 
 
-@pytest.mark.parametrize("scale", [1e-3, 30.0])
-def test_weight_scales(scale):
-    """Per-layer power-of-two weight scaling: a net with every Linear weight x 1e-3 (lo terms would be fp16
-    subnormals unscaled) or x 30 (hi terms near the fp16 range unscaled) still meets the oracle at the bar."""
-    B, H, d, C, N = 128, 32, 2, 4, 100
-    net = make_mlp(d, H, C, seed=7)
-    with torch.no_grad():
-        for m in net.modules():
-            if isinstance(m, torch.nn.Linear):
-                m.weight.mul_(scale if m.weight.shape[0] != H * d else 1.0)
+def _oracle_and_gpu(net, d, H, C, N, B, seed=11):
     plan = _plan(net, d, H, C, N)
     ctx = _ctx(C)
-    noise = torch.randn(N + 1, B, H, d, generator=torch.Generator().manual_seed(11))
+    noise = torch.randn(N + 1, B, H, d, generator=torch.Generator().manual_seed(seed))
     ref = osam.ddpm_cfg(net, osch.buffers("exponential", N), ctx.expand(B, C), 0.01, B, H, noise=noise,
                         return_chain=True)
     got = plan.run_CFG(ctx, None, 0.01, n_samples=B, horizon=H, return_chain=True, noise=noise)
-    if not torch.isfinite(ref).all():
-        pytest.skip("the oracle itself overflows at this scale")
-    if not torch.isfinite(got).all():
-        # activations beyond the fp16 range: reported as non-finite, never silently wrong
-        amax = torch.empty(B, dtype=torch.float32, device=plan.device)
-        plan.sample_trajectories(ctx, B, H, noise=noise, absmax_out=amax)
-        assert torch.isnan(amax).any() or torch.isinf(amax).any()
-        return
-    assert_traj_close(got, ref, what=f"f16x2, weights x {scale}")
+    torch.cuda.synchronize()
+    return plan, ref, got
+
+
+def _scaled_mlp(d, H, C, seed, weight=1.0, first=None, bias=None):
+    """make_mlp with every Linear weight x `weight` but the final layer's (first: the input layer's factor instead;
+    bias: every Linear bias x `bias`)"""
+    net = make_mlp(d, H, C, seed=seed)
+    lins = [m for m in net.modules() if isinstance(m, torch.nn.Linear)]
+    with torch.no_grad():
+        for m in lins:
+            if m.weight.shape[0] == H * d:
+                continue  # the final Linear (flat output)
+            f = first if (first is not None and m.weight.shape[1] == H * d) else (weight if first is None else 1.0)
+            m.weight.mul_(f)
+            if bias is not None:
+                m.bias.mul_(bias)
+    return net
+
+
+@pytest.mark.parametrize("scale", [1e-3, 30.0])
+def test_weight_scales(scale):
+    """Per-layer power-of-two weight scaling: a net with every Linear weight x 1e-3 (lo terms would be fp16
+    subnormals unscaled) or x 30 (hi terms near the fp16 range unscaled) meets the oracle at the bar - a hard
+    assertion: an f16x2 call that leaves the fp16 range is re-run with the net's split-bf16 kernels (planner)."""
+    B, H, d, C, N = 128, 32, 2, 4, 100
+    plan, ref, got = _oracle_and_gpu(_scaled_mlp(d, H, C, 7, weight=scale), d, H, C, N, B)
+    assert torch.isfinite(ref).all(), "the oracle itself must stay finite at this scale"
+    assert torch.isfinite(got).all()
+    tr, el = assert_traj_close(got, ref, what=f"f16x2, weights x {scale}")
+    print(f"weights x {scale}: f32x3 re-run {plan.last_f32x3_rerun}, worst trajectory {tr:.3e}, element {el:.3e}")
+
+
+def test_large_activations():
+    """Input-layer weights x 100: first-layer activations two orders of magnitude up (|v| into the thousands)."""
+    B, H, d, C, N = 128, 32, 2, 4, 100
+    plan, ref, got = _oracle_and_gpu(_scaled_mlp(d, H, C, 8, first=100.0), d, H, C, N, B)
+    assert torch.isfinite(ref).all() and torch.isfinite(got).all()
+    tr, el = assert_traj_close(got, ref, what="f16x2, input layer x 100")
+    print(f"input layer x 100: f32x3 re-run {plan.last_f32x3_rerun}, worst trajectory {tr:.3e}, element {el:.3e}")
+
+
+def test_small_activations():
+    """Biases zeroed and every hidden weight x 1e-2: activations shrink ~100x per layer, deep into the fp16 subnormal
+    range (absolute precision 2^-25 there); their contribution to eps shrinks with them."""
+    B, H, d, C, N = 128, 32, 2, 4, 100
+    plan, ref, got = _oracle_and_gpu(_scaled_mlp(d, H, C, 9, weight=1e-2, bias=0.0), d, H, C, N, B)
+    assert torch.isfinite(ref).all() and torch.isfinite(got).all()
+    tr, el = assert_traj_close(got, ref, what="f16x2, biases 0, weights x 1e-2")
+    print(f"small activations: f32x3 re-run {plan.last_f32x3_rerun}, worst trajectory {tr:.3e}, element {el:.3e}")
+
+
+def test_out_of_range_reruns_in_f32x3():
+    """A net whose activations certainly leave the fp16 range (hidden weights x 1e4, final layer x 1e-8 so the oracle's
+    eps stays moderate): the f16x2 chain would hold NaN; the planner re-runs the call with the split-bf16 kernels
+    (bit-identical to an f32x3 plan of the same weights), and mpcd_mpc_step does the same by itself
+    (MPCD_STEP_F32X3_RERUN)."""
+    from mpc_via_diffusion_model_amd import _native as N_
+    from mpc_via_diffusion_model_amd import systems
+    B, H, d, C, N = 64, 32, 2, 4, 50
+    net = _scaled_mlp(d, H, C, 10, first=1e4)
+    with torch.no_grad():
+        lins = [m for m in net.modules() if isinstance(m, torch.nn.Linear)]
+        lins[-1].weight.mul_(1e-8)
+    plan = _plan(net, d, H, C, N)
+    ref_plan = _plan(net, d, H, C, N, dtype="f32x3")
+    ctx = _ctx(C)
+    got = plan.sample_trajectories(ctx, B, H, seed=4)
+    assert plan.last_f32x3_rerun, "the f16x2 kernel should have left the fp16 range here"
+    want = ref_plan.sample_trajectories(ctx, B, H, seed=4)
+    torch.cuda.synchronize()
+    assert torch.isfinite(got).all() and torch.equal(got, want)
+    x0 = np.random.default_rng(1).uniform(-1, 1, C)
+    r = plan.mpc_step(x0, systems.get("double_int2d"), B, w=0.01, seed=6)
+    r_ref = ref_plan.mpc_step(x0, systems.get("double_int2d"), B, w=0.01, seed=6)
+    assert r.flags & N_.MPCD_STEP_F32X3_RERUN and not (r_ref.flags & N_.MPCD_STEP_F32X3_RERUN)
+    assert r.best_index == r_ref.best_index and r.best_cost == r_ref.best_cost
+    assert torch.equal(r.u_norm, r_ref.u_norm)

@@ -133,10 +133,11 @@ def test_reference_ddim_temporal_unet():
     assert_traj_close(got[: ref.shape[0]], ref, spread=spread, what="ddim TemporalUnet")
 
 
-@pytest.mark.parametrize("dtype", FP32_KINDS)
+@pytest.mark.parametrize("dtype", FP32_KINDS + ["f16x2"])
 def test_kat3_trained_checkpoint_on_gpu(dtype):
     """trained cart_pole_84000_test1 EMA weights + the checkpoint's own schedule
-    buffers; torch.manual_seed(0) context/noise stream; final u[0:8] to 4 decimals."""
+    buffers; torch.manual_seed(0) context/noise stream; final u[0:8] to 4 decimals. f16x2: the two-term fp16 fused
+    program (22-bit operands) against the same printed decimals."""
     from safetensors.torch import load_file
     sd = load_file(os.path.join(HERE, "golden", "cart_pole_84000_test1_ema.safetensors"))
     plan = DiffusionMPC.from_state_dict(sd, NetSpec("unet", state_dim=1, horizon=32, context_dim=5, dtype=dtype))

@@ -104,6 +104,13 @@ run_job() {
   esac
 }
 
+# refuse a library older than its sources (a snapshot taken before the rebuild finished)
+for f in mpc_via_diffusion_model_amd/csrc/* include/mpcd.h; do
+  if [ "$f" -nt mpc_via_diffusion_model_amd/libmpcd.so ]; then
+    echo "[gpu.sh] STALE libmpcd.so: $f is newer; rebuild before the call" >&2
+    exit 3
+  fi
+done
 rocminfo 2>/dev/null | grep -m2 -E "gfx950|Marketing" > gpurun_out/rocminfo.txt
 for j in "$@"; do
   echo "[gpu.sh] $j $(date +%T)"
