@@ -323,7 +323,11 @@ typedef struct {
     double *costs_all;             /* dev [nranks * batch] all costs (out), needed with a communicator, else unused */
 } mpcd_step_args;
 
-/* best_host: global winner (index over all ranks); u_best_host: host [H*d] fp32, the winner's
+/* Ordering: best_host / u_best_host are complete when the call returns (one rank: the call spins on a completion word
+ * the selecting workgroup writes to mapped host memory after the result block; with a communicator: a stream
+ * synchronisation). The DEVICE outputs (sample.x_out, cost_local, costs_all) are ordered only on hip_stream: read them
+ * from another stream or from the host after a stream synchronisation or an event.
+ * best_host: global winner (index over all ranks); u_best_host: host [H*d] fp32, the winner's
  * UNnormalised trajectory (u_best[0] is the applied action before the reference's rounding).
  * Returns MPCD_ENONFINITE (outputs written) when the winning cost is not finite, i.e. every candidate of
  * every rank is NaN / Inf - garbage is never returned as a normal result. */

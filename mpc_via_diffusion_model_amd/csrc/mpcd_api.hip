@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <thread>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -1181,7 +1182,9 @@ static int mpc_step_impl(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_h
         c->step_host = nullptr;
         c->step_host_dev = nullptr;
         c->step_host_bytes = 0;
-        HIP_TRY(hipHostMalloc(&c->step_host, host_bytes, hipHostMallocDefault));
+        // coherent (fine-grained) mapped memory: the selecting workgroup's system-scope stores of the result block
+        // and the completion word reach the host without depending on HIP_HOST_COHERENT's default
+        HIP_TRY(hipHostMalloc(&c->step_host, host_bytes, hipHostMallocMapped | hipHostMallocCoherent));
         HIP_TRY(hipHostGetDevicePointer(&c->step_host_dev, c->step_host, 0));
         memset(c->step_host, 0, host_bytes);
         c->step_seq = 0;
@@ -1274,7 +1277,11 @@ static int mpc_step_impl(mpcd_ctx *c, const mpcd_step_args *a, mpcd_best *best_h
                     return fail(MPCD_EHIP, "mpcd_mpc_step: the stream finished without the result block");
                 if (q != hipSuccess && q != hipErrorNotReady) HIP_TRY(q);
             }
-            __builtin_ia32_pause();
+#if defined(__x86_64__) || defined(__i386__)
+            __builtin_ia32_pause();  // spin-wait hint (host CPU)
+#else
+            std::this_thread::yield();
+#endif
         }
         std::atomic_thread_fence(std::memory_order_acquire);
     }

@@ -934,10 +934,13 @@ int sample_fused(const mpcd_net_desc &d, const UnetWeights &W, const UnetSampleA
         }
         hipError_t e = unet_fused_step(pl, f, st);
         if (e != hipSuccess) return uerr(MPCD_EHIP, std::string("fused U-Net: ") + hipGetErrorString(e));
-        if (split)
+        if (split) {
             hipLaunchKernelGGL(update_kernel, dim3(g1), dim3(threads), 0, st, xs, eps_buf, a.batch, flat, a.plan, s, a.mode,
                                a.clamp_x0, a.wp1, a.wf, a.noise, a.seed, a.global_offset, a.chain, a.x_out,
                                s == a.n_steps - 1 ? 1 : 0, amq);
+            if ((e = hipGetLastError()) != hipSuccess)
+                return uerr(MPCD_EHIP, std::string("fused U-Net update: ") + hipGetErrorString(e));
+        }
     }
     if (prof) {
         std::vector<uint64_t> h(prof_n);

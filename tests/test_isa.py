@@ -70,31 +70,37 @@ def test_every_mfma_source_two_wait_states_after_a_valu_write(tmp_path):
     assert not bad, f"{len(bad)} MFMA sources written by a VALU op under 2 wait states: {bad[:3]}"
 
 
-def test_asm_mfma_results_wait_before_valu_reads(tmp_path):
-    """The other direction for the inline-asm MFMAs (AGPR operands): a VALU op may read an MFMA result - or overwrite
-    it (write after write; in these in-place chains also the write after the in-flight MFMA's srcC read) - only as
-    many wait states after it as hipcc leaves after the builtin v_mfma_f32_16x16x32_bf16 (its minimum over the whole
-    library is the toolchain's requirement: 8 today, which the asm statements of csrc/mlp_rw.hip write out). If a
-    toolchain raises that requirement, the asm waits fall under it and this fails."""
+@pytest.mark.parametrize("op,kernel", [("v_mfma_f32_16x16x32_bf16", "mlp_rw_kernel"),
+                                       ("v_mfma_f32_16x16x32_f16", "mlp_h2_kernel")])
+def test_asm_mfma_results_wait_before_valu_reads(tmp_path, op, kernel):
+    """The other direction for the inline-asm MFMAs (AGPR operands; csrc/mlp_rw.hip bf16, csrc/mlp_h2.hip f16): a VALU
+    op may read an MFMA result - or overwrite it (write after write; in these in-place chains also the write after
+    the in-flight MFMA's srcC read) - only as many wait states after it as hipcc leaves after the builtin form of the
+    same opcode (its minimum over the whole library is the toolchain's requirement: 8 today for both, which the asm
+    statements write out as s_nop 7). If a toolchain raises that requirement, the asm waits fall under it and this
+    fails."""
     import mfma_hazard as mh
-    acc = mh.result_reads(_disassemble(tmp_path))
-    bf16 = [r for r in acc if r[1].startswith("v_mfma_f32_16x16x32_bf16")]
-    builtin = [r for r in bf16 if ", a[" not in r[1]]
-    asm = [r for r in bf16 if ", a[" in r[1]]
-    assert builtin and asm, "expected both builtin and AGPR-operand bf16 MFMAs"
+    lines = _disassemble(tmp_path)
+    acc = mh.result_reads(lines)
+    rs = [r for r in acc if r[1].startswith(op)]
+    builtin = [r for r in rs if ", a[" not in r[1]]
+    asm = [r for r in rs if ", a[" in r[1]]
+    assert builtin and asm, f"expected both builtin and AGPR-operand {op} MFMAs"
+    assert any(kernel in r[0] for r in asm), f"no AGPR-operand {op} in {kernel}"
     req = min(r[3] for r in builtin if r[4] == "read")
-    assert req == 8, f"hipcc's own wait after the bf16 MFMA is now {req} (was 8): revisit mlp_rw.hip's s_nop 7"
+    assert req == 8, f"hipcc's own wait after {op} is now {req} (was 8): revisit the asm statements' s_nop 7"
     close = [r for r in asm if r[3] < req]
-    assert not close, (f"{len(close)} VALU accesses of an asm MFMA result under {req} wait states "
+    assert not close, (f"{len(close)} VALU accesses of an asm {op} result under {req} wait states "
                        f"(reads {sum(r[4] == 'read' for r in close)}, writes {sum(r[4] == 'write' for r in close)}): "
                        f"{close[:3]}")
 
 
-def test_result_scan_reports_close_reads_and_writes():
+@pytest.mark.parametrize("op", ["v_mfma_f32_16x16x32_bf16", "v_mfma_f32_16x16x32_f16"])
+def test_result_scan_reports_close_reads_and_writes(op):
     import mfma_hazard as mh
-    asm = ["_Z1kv:", "  v_mfma_f32_16x16x32_bf16 v[28:31], a[20:23], v[0:3], v[28:31]", "  s_nop 3",
+    asm = ["_Z1kv:", f"  {op} v[28:31], a[20:23], v[0:3], v[28:31]", "  s_nop 3",
            "  v_mov_b32_e32 v29, v33",
-           "  v_mfma_f32_16x16x32_bf16 v[8:11], a[20:23], v[0:3], v[8:11]", "  s_nop 1",
+           f"  {op} v[8:11], a[20:23], v[0:3], v[8:11]", "  s_nop 1",
            "  v_add_f32_e32 v40, v9, v9"]
     got = [(r[2].split()[0], r[3], r[4]) for r in mh.result_reads(asm)]
     assert got == [("v_mov_b32_e32", 4, "write"), ("v_add_f32_e32", 2, "read")], got
