@@ -42,24 +42,6 @@ MPCD_DEV float mish_scalar(float x)
     return y;
 }
 
-// Mish in log2 units, for the split-bf16 MLP samplers (mlp_x3.hip / mlp_rw.hip), whose pack scales Linear 0's weights
-// and every hidden bias by log2(e) (and Linear 13's weights by 1/log2(e)), so that each hidden accumulator holds
-// a = log2(e) * x and each stored activation log2(e) * Mish(x): the same operations as mish() but the first product
-// (one VALU op per activation). mish_l2(a) = log2(e) * Mish(a / log2(e)).
-MPCD_DEV float mish_l2(float a)
-{
-    const float n = __builtin_amdgcn_exp2f(a);
-    const float r = __builtin_amdgcn_rcpf(__builtin_fmaf(n, n + 2.0f, 2.0f));
-    return a * __builtin_fmaf(-2.0f, r, 1.0f);
-}
-MPCD_DEV float mish_l2_scalar(float a)
-{
-    float y = mish_l2(a);
-    asm volatile("" : "+v"(y));
-    return y;
-}
-constexpr float kLog2e = 1.44269504088896341f;
-
 // torch.clamp(x, -1, 1) / torch.clip: a NaN stays NaN (fminf / fmaxf alone would return the bound), so a
 // non-finite noise prediction propagates to the samples as in the reference instead of turning into -1.
 MPCD_DEV float clamp1(float x)

@@ -264,10 +264,10 @@ struct MlpRw {
             const int n = nt_of<l>(wave, j) * 16 + 4 * q;
             f32x4 v = acc[j][c];
             if (EPI != EPI_NONE) {
-                v.x = mish_l2_scalar(v.x);
-                v.y = mish_l2_scalar(v.y);
-                v.z = mish_l2_scalar(v.z);
-                v.w = mish_l2_scalar(v.w);
+                v.x = mish_scalar(v.x);
+                v.y = mish_scalar(v.y);
+                v.z = mish_scalar(v.z);
+                v.w = mish_scalar(v.w);
             }
             u32x2 p0, p1, p2;
             split3(v, p0, p1, p2);
@@ -342,7 +342,7 @@ struct MlpRw {
         // epilogue of pass p in five units: Mish of element 0..3, then the split + the three plane stores
         auto epi_unit = [&](int u, f32x4 &v, int p) {
             if (u < 4) {
-                if (EPI != EPI_NONE) v[u] = mish_l2_scalar(v[u]);
+                if (EPI != EPI_NONE) v[u] = mish_scalar(v[u]);
                 return;
             }
             const int n = nt_of<l>(wave, jp(p)) * 16 + 4 * q;
@@ -372,7 +372,7 @@ struct MlpRw {
             if (EPI != EPI_NONE && k < 16) {
                 const int e = k & 3;
                 switch (k >> 2) {
-                case 0: et[e] = __builtin_amdgcn_exp2f(ev[e]); fence(et[e]); break;  // log2 units (mish_l2)
+                case 0: et[e] = __builtin_amdgcn_exp2f(ev[e] * 1.44269504088896341f); fence(et[e]); break;
                 case 1: et[e] = __builtin_fmaf(et[e], et[e] + 2.0f, 2.0f); fence(et[e]); break;
                 case 2: et[e] = __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(et[e]), 1.0f); fence(et[e]); break;
                 default: { float y = ev[e] * et[e]; fence(y); ev[e] = y; } break;
@@ -837,10 +837,8 @@ struct MlpRw {
             if (threadIdx.x < COND_TOTAL / 2) {
                 const bool ctx_half = threadIdx.x >= COND_TOTAL / 4;
                 const int k = ctx_half ? (int)threadIdx.x - COND_TOTAL / 4 : (int)threadIdx.x;
-                // log2 units (mish_l2): the pack's cond biases are scaled already, the projections here (the
-                // operations of mlp_x3.hip's table)
-                f32x4 u = tpre * kLog2e + reinterpret_cast<const f32x4 *>(lds + L::BIC)[k];
-                if (ctx_half) u = u + reinterpret_cast<const f32x4 *>(lds + L::CPS)[k] * kLog2e;
+                f32x4 u = tpre + reinterpret_cast<const f32x4 *>(lds + L::BIC)[k];
+                if (ctx_half) u = u + reinterpret_cast<const f32x4 *>(lds + L::CPS)[k];
                 reinterpret_cast<f32x4 *>(lds + (ctx_half ? L::TPC : L::TPU))[k] = u;
             }
             tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 1 < p.n_steps ? s + 1 : s) * COND_TOTAL)[tpi];

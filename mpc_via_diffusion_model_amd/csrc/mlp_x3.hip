@@ -99,10 +99,10 @@ struct MlpX3 {
             const int n = ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q;
             f32x4 v = acc[j][c];
             if (EPI != EPI_NONE) {
-                v.x = mish_l2_scalar(v.x);
-                v.y = mish_l2_scalar(v.y);
-                v.z = mish_l2_scalar(v.z);
-                v.w = mish_l2_scalar(v.w);
+                v.x = mish_scalar(v.x);
+                v.y = mish_scalar(v.y);
+                v.z = mish_scalar(v.z);
+                v.w = mish_scalar(v.w);
             }
             u32x2 p0, p1, p2;
             split3(v, p0, p1, p2);
@@ -169,10 +169,10 @@ struct MlpX3 {
             const int n = ntile_of<K, N, MODE>(wave, j) * 16 + 4 * q;
             f32x4 v = acc[j][c];
             if (EPI != EPI_NONE) {
-                v.x = mish_l2_scalar(v.x);
-                v.y = mish_l2_scalar(v.y);
-                v.z = mish_l2_scalar(v.z);
-                v.w = mish_l2_scalar(v.w);
+                v.x = mish_scalar(v.x);
+                v.y = mish_scalar(v.y);
+                v.z = mish_scalar(v.z);
+                v.w = mish_scalar(v.w);
             }
             u32x2 p0, p1, p2;
             split3(v, p0, p1, p2);
@@ -462,10 +462,9 @@ struct MlpX3 {
             bar(0);
             // this step's time projections + cond biases (+ shared context part) -> TPU / TPC
             if (threadIdx.x < COND_TOTAL / 4) {
-                // log2 units (mish_l2): the pack's cond biases are scaled already, the projections here
-                const f32x4 u = tpre * kLog2e + reinterpret_cast<const f32x4 *>(lds + L::BIC)[tpi];
+                const f32x4 u = tpre + reinterpret_cast<const f32x4 *>(lds + L::BIC)[tpi];
                 reinterpret_cast<f32x4 *>(lds + L::TPU)[tpi] = u;
-                reinterpret_cast<f32x4 *>(lds + L::TPC)[tpi] = u + reinterpret_cast<const f32x4 *>(lds + L::CPS)[tpi] * kLog2e;
+                reinterpret_cast<f32x4 *>(lds + L::TPC)[tpi] = u + reinterpret_cast<const f32x4 *>(lds + L::CPS)[tpi];
             }
             tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 1 < p.n_steps ? s + 1 : s) * COND_TOTAL)[tpi];
             layer<0>(w0, lds, wave, lane);
@@ -677,12 +676,8 @@ static float bf16_val(uint16_t h)
     return f;
 }
 
-// Log2 units (common.h mish_l2): Linear 0's weights and the biases of Linear 0..12 are stored x log2(e), Linear 13's
-// weights / log2(e) (each product rounded once from fp64), so every hidden accumulator is log2(e) x the reference's
-// pre-activation and the epilogue's exp2 needs no multiply; the eps of Linear 13 comes out unscaled.
 void mlp_pack_weights_x3(int d0, const float *const *lin_w, const float *const *lin_b, float *out)
 {
-    const double L2E = 1.4426950408889634074;
     const int Ks[NLAYER] = {d0, 32, 32, 64, 64, 128, 128, 128, 256, 64, 128, 32, 32, 32};
     const int Ns[NLAYER] = {32, 32, 64, 64, 128, 128, 128, 128, 64, 64, 32, 32, 32, d0};
     size_t o = 0;  // in floats
@@ -693,8 +688,7 @@ void mlp_pack_weights_x3(int d0, const float *const *lin_w, const float *const *
             for (int kc = 0; kc < KC; ++kc)
                 for (int lane = 0; lane < 64; ++lane)
                     for (int j = 0; j < 8; ++j) {
-                        const float w0 = lin_w[l][(size_t)(nt * 16 + (lane & 15)) * K + kc * 32 + 8 * (lane >> 4) + j];
-                        const float w = l == 0 ? (float)(w0 * L2E) : l == NLAYER - 1 ? (float)(w0 / L2E) : w0;
+                        const float w = lin_w[l][(size_t)(nt * 16 + (lane & 15)) * K + kc * 32 + 8 * (lane >> 4) + j];
                         if (WPL == 2) {  // fp32 as loaded; the kernel splits it (to_planes)
                             out[o + ((size_t)(nt * KC + kc) * 64 + lane) * 8 + j] = w;
                             continue;
@@ -709,7 +703,7 @@ void mlp_pack_weights_x3(int d0, const float *const *lin_w, const float *const *
                             pk[(((size_t)(nt * KC + kc) * 3 + pl) * 64 + lane) * 8 + j] = hs[pl];
                     }
         o += (size_t)WPL * K * N / 2;
-        for (int n = 0; n < N; ++n) out[o + n] = l < NLAYER - 1 ? (float)(lin_b[l][n] * L2E) : lin_b[l][n];
+        for (int n = 0; n < N; ++n) out[o + n] = lin_b[l][n];
         o += N;
     }
 }
