@@ -52,13 +52,14 @@ def assert_traj_close(got, ref, rel=REL_TRAJ, abs_elem=ABS_ELEM, what="", spread
 
 
 # elementwise bar of an ill-conditioned chain (unclamped DDIM, the trained 30-step Panda / LMPC chains): this multiple
-# of the oracle's own spread when its layers round from fp64 (oracle_sensitivity). Another fp32-accurate implementation
-# (split-bf16 GEMMs, its own reduction orders) lands a small multiple of that spread away: at most 2.89x in round 4
-# (profiles/r4_spread_ratios.tsv: MLP DDIM 2.89, MLP CFG-DDIM 2.36, fused U-Net CFG-DDIM 2.11, Panda 2.02, LMPC 1.81;
-# this round's record: profiles/r5_spread_ratios.tsv). 4 keeps >= 25 % headroom over that maximum. The oracle's own
-# spread under four seeded random half-ulp roundings of every layer is larger still (up to 34x the fp64 spread on
-# the MLP DDIM chain), so the bar stays anchored on the tightest perturbation; the trajectory bar (1e-4) is not relaxed.
-SPREAD_X = 4
+# of the oracle's own spread when its layers round from fp64 instead of fp32 (oracle_sensitivity: ONE perturbation,
+# the bar's anchor). Another fp32-accurate implementation (split-bf16 GEMMs, its own reduction orders) lands a small
+# multiple of that spread away: at most 2.89x over every recorded chain, the two-term fp16 ones included
+# (profiles/r6_spread_ratios.tsv: MLP DDIM 2.89, MLP CFG-DDIM 2.36, LMPC 1.81, Panda f32 2.02 / f16x2 1.38, cfg3 full
+# batch 0.33). The oracle's spread under four seeded random half-ulp roundings of every layer (MPCD_SPREAD_LOG
+# records it beside the anchor, it is not the bar) is larger still on most chains; the trajectory bar (1e-4) is not
+# relaxed.
+SPREAD_X = 3
 SENSITIVITY_SEEDS = (1, 2, 3, 4)
 
 
