@@ -473,17 +473,32 @@ struct MlpRw {
     // bounded (2^16 sleeps): a lost signal gives a wrong result that the parity tests report, never a hang.
     // MPCD_RW_FLAGS = 0 keeps the workgroup barrier at every layer boundary of the 32-row form too (A/B builds)
 #ifndef MPCD_RW_FLAGS
-#define MPCD_RW_FLAGS 1
+#define MPCD_RW_FLAGS 0
 #endif
     static constexpr bool FLAGS = R == 32 && MPCD_RW_FLAGS;
+// experiment switches of the counter form (A/B builds): MPCD_RW_SIGWAIT 0 drops the lgkmcnt(0) before a signal (LDS
+// executes one wave's DS instructions in order), MPCD_RW_SLEEP 0 polls without s_sleep, MPCD_RW_CARRY 0 keeps every
+// layer's last epilogue in the layer
+#ifndef MPCD_RW_SIGWAIT
+#define MPCD_RW_SIGWAIT 1
+#endif
+#ifndef MPCD_RW_SLEEP
+#define MPCD_RW_SLEEP 1
+#endif
+#ifndef MPCD_RW_CARRY
+#define MPCD_RW_CARRY 1
+#endif
+    static constexpr bool CARRY = MPCD_RW_CARRY;
     static constexpr int CNT = L::total;
     static constexpr int LDS_BYTES = L::total + (R == 32 ? 32 * 4 : 0);
     static MPCD_DEV void flag_signal(char *lds, int l, int c, int lane)
     {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(lds + CNT) + 2 * l + c, 1u, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-        asm volatile("" ::: "memory");
+        // lane 0's ds_add_u32 as asm: the atomic builtin went through hipcc's atomic optimizer (a popcount of the
+        // active lanes by two v_mbcnt and a compare per signal)
+        typedef __attribute__((address_space(3))) uint32_t lds_u32;
+        const uint32_t addr = (uint32_t)(uintptr_t)((lds_u32 *)(reinterpret_cast<uint32_t *>(lds + CNT) + 2 * l + c));
+        if (MPCD_RW_SIGWAIT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) asm volatile("ds_add_u32 %0, %1" ::"v"(addr), "v"(1u) : "memory");
     }
     static MPCD_DEV void flag_wait(char *lds, int l, int c, uint32_t target)
     {
@@ -495,7 +510,7 @@ struct MlpRw {
             if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >=
                 target)
                 break;
-            __builtin_amdgcn_s_sleep(1);
+            if (MPCD_RW_SLEEP) __builtin_amdgcn_s_sleep(1);
         }
         asm volatile("" ::: "memory");
     }
@@ -1111,25 +1126,25 @@ struct MlpRw {
                 const uint32_t tgt = 4u * (uint32_t)(s + 1);
                 layer_f<1, NFRAG<4>>(w1, [&](int k) { load_ws1<4>(w4, ws, wave, lane16, k); }, cy, lds, wave, lane, tgt);
                 mark();
-                layer_f<2, 0, false, true>(w2, none, cy, lds, wave, lane, tgt);
+                layer_f<2, 0, false, CARRY>(w2, none, cy, lds, wave, lane, tgt);
                 mark();
-                layer_f<3, 0, true, true>(w3, none, cy, lds, wave, lane, tgt);
+                layer_f<3, 0, CARRY, CARRY>(w3, none, cy, lds, wave, lane, tgt);
                 mark();
-                layer_f<4, 0, true, true>(w4, none, cy, lds, wave, lane, tgt);
+                layer_f<4, 0, CARRY, CARRY>(w4, none, cy, lds, wave, lane, tgt);
                 mark();
-                layer_res_f<0, 0, true, true>(res, tail, none, cy, lds, wave, lane, tgt);
+                layer_res_f<0, 0, CARRY, CARRY>(res, tail, none, cy, lds, wave, lane, tgt);
                 mark();
-                layer_res_f<1, NFRAG<8>, true, true>(res, tail, [&](int k) { load_ws1<8>(w8, ws, wave, lane16, k); }, cy,
+                layer_res_f<1, NFRAG<8>, CARRY, CARRY>(res, tail, [&](int k) { load_ws1<8>(w8, ws, wave, lane16, k); }, cy,
                                                      lds, wave, lane, tgt);
                 load_tail(tail, ws, wave, lane16);
                 mark();
-                layer_res_f<2, 0, true, true>(res, tail, none, cy, lds, wave, lane, tgt);
+                layer_res_f<2, 0, CARRY, CARRY>(res, tail, none, cy, lds, wave, lane, tgt);
                 load_ws<9>(w9, ws, wave, lane16);
                 mark();
                 if (s + 1 < p.n_steps) sp = load_plan(p.plan, s + 1);
                 if constexpr (STAGED_NOISE) {
                     ph_init(ph, p, s + 2, cand0, wave, lane);  // step s + 1's noise is Philox slice s + 2 (fetch_noise)
-                    layer_f<8, NPH, true, true>(w8, [&](int k) { ph_step(ph, k); }, cy, lds, wave, lane, tgt);
+                    layer_f<8, NPH, CARRY, CARRY>(w8, [&](int k) { ph_step(ph, k); }, cy, lds, wave, lane, tgt);
                 } else {
                     layer_f<8, 0, true, true>(w8, none, cy, lds, wave, lane, tgt);
                 }
