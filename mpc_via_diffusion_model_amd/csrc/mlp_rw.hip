@@ -135,6 +135,17 @@ struct MlpRw {
     template <int l> static MPCD_DEV int nt_of(int wave, int j) { return SPL<l> ? (wave & 1) : wave + 4 * j; }
     template <int l> static MPCD_DEV int ct_of(int wave, int c) { return SPL<l> ? (wave >> 1) : c; }
 
+    // ONE buffer descriptor over the whole weight pack for every streamed layer (the layer offset goes into the
+    // soffset): per-layer descriptors, kept live across the step loop, cost 4 SGPRs each and pushed ~50 SGPRs into
+    // VGPR lanes (a v_readlane per use)
+    static MPCD_DEV __amdgpu_buffer_rsrc_t pack_rsrc(const float *__restrict__ wp)
+    {
+        const uint64_t a = (uint64_t)wp;
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+        return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(woffx<D0>(NLAYER) * 4),
+                                                 0x00020000);
+    }
+
     // streamed fragments of layer l for this wave
     template <int l>
     struct WS {
@@ -145,10 +156,7 @@ struct MlpRw {
     static MPCD_DEV void load_ws(WS<l> &f, const float *__restrict__ wp, int wave, int lane16)
     {
         constexpr int K = A::K[l], N = A::N[l], KC = K / 32, NT = N / 16;
-        const uint64_t a = (uint64_t)(wp + woffx<D0>(l));
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(3 * K * N * 2), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rs = pack_rsrc(wp);
 #pragma unroll
         for (int j = 0; j < TL<l>; ++j) {
             const int nt = min(nt_of<l>(wave, j), NT - 1);  // clamped: path-independent load count
@@ -156,7 +164,7 @@ struct MlpRw {
             for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl) {
-                    const int soff = __builtin_amdgcn_readfirstlane(((nt * KC + kc) * 3 + pl) * 1024);
+                    const int soff = __builtin_amdgcn_readfirstlane(woffx<D0>(l) * 4 + ((nt * KC + kc) * 3 + pl) * 1024);
                     f.v[j][kc][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
                 }
         }
@@ -168,13 +176,10 @@ struct MlpRw {
     static MPCD_DEV void load_ws1(WS<l> &w, const float *__restrict__ wp, int wave, int lane16, int f)
     {
         constexpr int K = A::K[l], N = A::N[l], KC = K / 32, NT = N / 16;
-        const uint64_t a = (uint64_t)(wp + woffx<D0>(l));
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(3 * K * N * 2), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rs = pack_rsrc(wp);
         const int j = f / (KC * 3), kc = (f / 3) % KC, pl = f % 3;
         const int nt = min(nt_of<l>(wave, j), NT - 1);
-        const int soff = __builtin_amdgcn_readfirstlane(((nt * KC + kc) * 3 + pl) * 1024);
+        const int soff = __builtin_amdgcn_readfirstlane(woffx<D0>(l) * 4 + ((nt * KC + kc) * 3 + pl) * 1024);
         w.v[j][kc][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
     }
     template <int l>
@@ -190,26 +195,20 @@ struct MlpRw {
     };
     static MPCD_DEV void load_tail1(Tail &t, const float *__restrict__ wp, int wave, int lane16, int f)
     {
-        const uint64_t a = (uint64_t)(wp + woffx<D0>(RES_L0 + RES_NL - 1));
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(3 * 128 * 128 * 2), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rs = pack_rsrc(wp);
         const int g = RES_AG + f / 3, pl = f % 3, j = (g / 4) & 1, kc = g & 3, nt = wave + 4 * j;
-        const int soff = __builtin_amdgcn_readfirstlane(((nt * 4 + kc) * 3 + pl) * 1024);
+        const int soff = __builtin_amdgcn_readfirstlane(woffx<D0>(RES_L0 + RES_NL - 1) * 4 + ((nt * 4 + kc) * 3 + pl) * 1024);
         t.v[g - RES_AG][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
     }
     static MPCD_DEV void load_tail(Tail &t, const float *__restrict__ wp, int wave, int lane16)
     {
-        const uint64_t a = (uint64_t)(wp + woffx<D0>(RES_L0 + RES_NL - 1));
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(3 * 128 * 128 * 2), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rs = pack_rsrc(wp);
 #pragma unroll
         for (int g = RES_AG; g < RES_G; ++g) {
             const int j = (g / 4) & 1, kc = g & 3, nt = wave + 4 * j;
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl) {
-                const int soff = __builtin_amdgcn_readfirstlane(((nt * 4 + kc) * 3 + pl) * 1024);
+                const int soff = __builtin_amdgcn_readfirstlane(woffx<D0>(RES_L0 + RES_NL - 1) * 4 + ((nt * 4 + kc) * 3 + pl) * 1024);
                 t.v[g - RES_AG][pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane16, soff, 0));
             }
         }
@@ -493,12 +492,13 @@ struct MlpRw {
     static constexpr int LDS_BYTES = L::total + (R == 32 ? 32 * 4 : 0);
     static MPCD_DEV void flag_signal(char *lds, int l, int c, int lane)
     {
-        // lane 0's ds_add_u32 as asm: the atomic builtin went through hipcc's atomic optimizer (a popcount of the
-        // active lanes by two v_mbcnt and a compare per signal)
-        typedef __attribute__((address_space(3))) uint32_t lds_u32;
-        const uint32_t addr = (uint32_t)(uintptr_t)((lds_u32 *)(reinterpret_cast<uint32_t *>(lds + CNT) + 2 * l + c));
+        // lane 0's ds_add_u32 (build.py compiles this file without hipcc's atomic optimizer, which turned it into a
+        // popcount of the active lanes - two v_mbcnt and a compare per signal)
         if (MPCD_RW_SIGWAIT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) asm volatile("ds_add_u32 %0, %1" ::"v"(addr), "v"(1u) : "memory");
+        if (lane == 0)
+            __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(lds + CNT) + 2 * l + c, 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        asm volatile("" ::: "memory");
     }
     static MPCD_DEV void flag_wait(char *lds, int l, int c, uint32_t target)
     {
@@ -848,11 +848,17 @@ struct MlpRw {
                     const float xv = x[r];
                     float o;
                     if (IS_DDPM) {
-                        const float x0c = sp.a * xv - sp.b * ec[r];
-                        const float x0u = sp.a * xv - sp.b * eu[r];
+                        // every intermediate through a fence: the SLP vectorizer paired the four values' products
+                        // into v_pk_mul / v_pk_add_f32, dearer than the plain ops here (same values either way)
+                        auto fn = [](float &v) { asm volatile("" : "+v"(v)); };
+                        float x0c = sp.a * xv - sp.b * ec[r];
+                        fn(x0c);
+                        float x0u = sp.a * xv - sp.b * eu[r];
+                        fn(x0u);
                         float x0 = p.wp1 * x0c - p.wf * x0u;
                         x0 = clamp1(x0);
-                        const float mean = sp.c1 * x0 + sp.c2 * xv;
+                        float mean = sp.c1 * x0 + sp.c2 * xv;
+                        fn(mean);
                         o = (sp.flags & PLAN_NOISE) ? mean + sp.std * nz[j][0][r] : mean;
                     } else if (SMODE == MODE_DDIM_CFG) {
                         float x0 = p.wp1 * (sp.a * xv - sp.b * ec[r]) - p.wf * (sp.a * xv - sp.b * eu[r]);
