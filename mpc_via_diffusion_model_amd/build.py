@@ -21,10 +21,7 @@ SOURCES = ["mpcd_api.hip", "comm.hip", "mlp_sampler.hip", "mlp_x3.hip", "mlp_rw.
 # f32 MFMA and VALU share issue on gfx950, so those moves cost MFMA time).
 # per-source additions. mlp_x3.hip: the memory-clause machine scheduler groups each layer's weight / LDS
 # fragment loads ahead of the MFMA chains (measured: cfg2 sampler 1.243 -> 1.205 ms; no effect on unet_mx)
-SOURCE_FLAGS = {"mlp_x3.hip": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
-                # mlp_rw.hip: its LDS counters take one lane's ds_add_u32 as written (the atomic optimizer would add a
-                # popcount of the active lanes to every signal)
-                "mlp_rw.hip": ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]}
+SOURCE_FLAGS = {"mlp_x3.hip": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]}
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}", "-mllvm", "-amdgpu-mfma-vgpr-form", "-Wall",
          "-Wno-unused-function", "-Wno-unused-variable"]
 

@@ -452,239 +452,6 @@ struct MlpRw {
 #endif
     }
 
-    // ---- 32 rows: the layer boundaries 1 -> 2 ... 11 -> 12 by per-(layer, column tile) LDS counters instead of
-    // workgroup barriers. A layer's column tile c (rows 16c .. 16c + 15) needs only column tile c of the layer before,
-    // so each wave runs its column-0 passes first, signals (l, 0) once their epilogue is stored and starts layer l + 1's
-    // column-0 passes as soon as every wave has signalled (l, 0) - while the column-1 work of layer l may still be in
-    // flight elsewhere. Between two layers of N >= 64 the last pass's epilogue (column tile 1) is not run at the end of
-    // layer l but CARRIED into layer l + 1, as micro-steps between its first (column-0) pass's MFMAs, and (l, 1) is
-    // signalled after its last store: the layer tail that the barrier form exposes (Mish, split and stores of the last
-    // pass, then the barrier and the next layer's first operand reads) runs under MFMAs. Same products, same order,
-    // same epilogue operations as hidden_ilv: bit-identical results. The SPL layers (N = 32: one pass per wave, column
-    // tile wave >> 1) take and give no carry (a carry of the column tile a wave itself needs first would wait on
-    // itself). Layer 0 -> 1 (layer 1 overwrites the x planes layer 0 reads for BOTH column tiles) and 12 -> final
-    // (the final layer pairs the two column tiles) keep their barriers.
-    //
-    // Counters: uint32 [16][2] after the Lds3 layout, zeroed before the first barrier, +1 per wave per step: every wave
-    // signals every (l, c), l = 1..11, once per step (a column tile it does not compute right at the layer start), so
-    // step s's target is 4 (s + 1). Release: s_waitcnt lgkmcnt(0) (this wave's stores are in LDS) before lane 0's
-    // ds_add; acquire: the polling read's value decides, in program order, before any read of the tile. The poll is
-    // bounded (2^16 sleeps): a lost signal gives a wrong result that the parity tests report, never a hang.
-    // MPCD_RW_FLAGS = 0 keeps the workgroup barrier at every layer boundary of the 32-row form too (A/B builds)
-#ifndef MPCD_RW_FLAGS
-#define MPCD_RW_FLAGS 0
-#endif
-    static constexpr bool FLAGS = R == 32 && MPCD_RW_FLAGS;
-// experiment switches of the counter form (A/B builds): MPCD_RW_SIGWAIT 0 drops the lgkmcnt(0) before a signal (LDS
-// executes one wave's DS instructions in order), MPCD_RW_SLEEP 0 polls without s_sleep, MPCD_RW_CARRY 0 keeps every
-// layer's last epilogue in the layer
-#ifndef MPCD_RW_SIGWAIT
-#define MPCD_RW_SIGWAIT 1
-#endif
-#ifndef MPCD_RW_SLEEP
-#define MPCD_RW_SLEEP 1
-#endif
-#ifndef MPCD_RW_CARRY
-#define MPCD_RW_CARRY 1
-#endif
-    static constexpr bool CARRY = MPCD_RW_CARRY;
-    static constexpr int CNT = L::total;
-    static constexpr int LDS_BYTES = L::total + (R == 32 ? 32 * 4 : 0);
-    static MPCD_DEV void flag_signal(char *lds, int l, int c, int lane)
-    {
-        // lane 0's ds_add_u32 (build.py compiles this file without hipcc's atomic optimizer, which turned it into a
-        // popcount of the active lanes - two v_mbcnt and a compare per signal)
-        if (MPCD_RW_SIGWAIT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0)
-            __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(lds + CNT) + 2 * l + c, 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-        asm volatile("" ::: "memory");
-    }
-    static MPCD_DEV void flag_wait(char *lds, int l, int c, uint32_t target)
-    {
-        // a relaxed atomic load (not a volatile one, which hipcc lowers to a flat load through a generic pointer):
-        // ds_read_b32, re-issued every poll
-        uint32_t *cnt = reinterpret_cast<uint32_t *>(lds + CNT) + 2 * l + c;
-#pragma nounroll
-        for (int it = 0; it < (1 << 16); ++it) {
-            if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >=
-                target)
-                break;
-            if (MPCD_RW_SLEEP) __builtin_amdgcn_s_sleep(1);
-        }
-        asm volatile("" ::: "memory");
-    }
-    struct Carry {
-        f32x4 ev;  // the pending pass's accumulators
-        int o;     // its output (plane 0): byte offset in LDS (a 32-bit LDS address, not a generic pointer)
-        int opl;   // plane stride of that buffer
-        int ct;    // its column tile
-    };
-    // epilogue micro-step k of 4 values v -> the three bf16 planes at o (plane stride opl): hidden_ilv's epi_step
-    struct EpiSt {
-        float et[4];
-        u32x2 ep0, ep1, ep2;
-        float er0, er1, er2, er3;
-    };
-    template <int EPI>
-    static constexpr int nstep() { return (EPI != EPI_NONE ? 16 : 0) + 8; }
-    template <int EPI>
-    static MPCD_DEV void epi_micro(int k, f32x4 &ev, EpiSt &e, char *o, int opl)
-    {
-        auto fence = [](float &x) { asm volatile("" : "+v"(x)); };
-        if (EPI != EPI_NONE && k < 16) {
-            const int i = k & 3;
-            switch (k >> 2) {
-            case 0: e.et[i] = __builtin_amdgcn_exp2f(ev[i] * 1.44269504088896341f); fence(e.et[i]); break;
-            case 1: e.et[i] = __builtin_fmaf(e.et[i], e.et[i] + 2.0f, 2.0f); fence(e.et[i]); break;
-            case 2: e.et[i] = __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(e.et[i]), 1.0f); fence(e.et[i]); break;
-            default: { float y = ev[i] * e.et[i]; fence(y); ev[i] = y; } break;
-            }
-            return;
-        }
-        switch (EPI != EPI_NONE ? k - 16 : k) {
-        case 0: e.ep0 = u32x2{pk_bf16(ev.x, ev.y), pk_bf16(ev.z, ev.w)}; break;
-        case 1: e.er0 = ev.x - bf_lo(e.ep0.x); fence(e.er0); e.er1 = ev.y - bf_hi(e.ep0.x); fence(e.er1); break;
-        case 2: e.er2 = ev.z - bf_lo(e.ep0.y); fence(e.er2); e.er3 = ev.w - bf_hi(e.ep0.y); fence(e.er3); *reinterpret_cast<u32x2 *>(o) = e.ep0; break;
-        case 3: e.ep1 = u32x2{pk_bf16(e.er0, e.er1), pk_bf16(e.er2, e.er3)}; break;
-        case 4: e.er0 = e.er0 - bf_lo(e.ep1.x); fence(e.er0); e.er1 = e.er1 - bf_hi(e.ep1.x); fence(e.er1); break;
-        case 5: e.er2 = e.er2 - bf_lo(e.ep1.y); fence(e.er2); e.er3 = e.er3 - bf_hi(e.ep1.y); fence(e.er3); break;
-        case 6: *reinterpret_cast<u32x2 *>(o + opl) = e.ep1; e.ep2 = u32x2{pk_bf16(e.er0, e.er1), pk_bf16(e.er2, e.er3)}; break;
-        default: *reinterpret_cast<u32x2 *>(o + 2 * opl) = e.ep2; break;
-        }
-    }
-
-    // Layer l (1..12) at 32 rows with counters (above). CIN: a carry from layer l - 1 is pending in cy (its epilogue
-    // runs in this layer's first pass); COUT: this layer's last pass is left pending in cy. tgt = 4 (s + 1).
-    template <int l, int NS, bool CIN, bool COUT, class MM1, class SIDE>
-    static MPCD_DEV void hidden_fl(MM1 mm1, SIDE side, Carry &cy, char *lds, int wave, int lane, uint32_t tgt)
-    {
-        constexpr int K = A::K[l], N = A::N[l], KC = K / 32, NT = N / 16, T = TL<l>, EPI = epi_of(l);
-        constexpr bool S = SPL<l>;
-        constexpr int NP = S ? 1 : 2 * T, NI = NP * KC;  // passes (column tile 0's, then column tile 1's)
-        constexpr bool WAIT = l >= 2, SIG = l <= 11;
-        static_assert(R == 32 && NCT == 2 && l >= 1 && l <= 12, "32-row layers 1..12");
-        static_assert(S || (T * 16 * 4 == N), "every wave owns T n-tiles of each column tile");
-        static_assert(!CIN || (!S && !SPL<l - 1> && l >= 2), "carries only between N >= 64 layers");
-        static_assert(!COUT || (!S && l + 1 <= 12 && !SPL<l + 1>), "carries only between N >= 64 layers");
-        constexpr int EPC = CIN ? epi_of(l - 1) : EPI_NONE;  // the carried pass's epilogue
-        constexpr int NSC = CIN ? nstep<EPC>() : 0, NSTEP = nstep<EPI>();
-        // the first column-1 pass may have its operands read ahead (two k-chunks, inside a column-0 pass) unless this
-        // wave's own carry - a column-1 tile of layer l - 1 - is still pending then (one n-tile per wave: T = 1)
-        constexpr bool CROSS = !CIN || T >= 2;
-        constexpr int I1 = S ? NI : T * KC;  // the first column-1 step
-        const int col = lane & 15, q = lane >> 4;
-        auto ctp = [&](int p) { return S ? (wave >> 1) : p / T; };       // column tile of pass p
-        auto ntp = [&](int p) { return S ? (wave & 1) : wave + 4 * (p % T); };
-        auto init_of = [&](int p) {
-            const int ct = ctp(p);
-            const float *init = reinterpret_cast<const float *>(
-                lds + (EPI == EPI_CMISH ? (masked_of(ct, col) ? L::TPU : L::TPC) + cond_off(l / 2) * 4
-                                        : L::BI + A::boff(l) * 4));
-            return *reinterpret_cast<const f32x4 *>(init + ntp(p) * 16 + 4 * q);
-        };
-        auto ldx = [&](u32x4 (&x)[3], int i) {
-            const int p = i / KC, kc = i % KC, row = ctp(p) * 16 + col;
-            load_x3(x, lds + L::in_off(l) + row * L::in_rs(l) + kc * 64 + 16 * (q ^ swz(row)), L::in_pl(l));
-        };
-        auto out_of = [&](int p) {
-            const int ro = ctp(p) * 16 + col;
-            return lds + L::out_off(l) + ro * L::out_rs(l) + st_off(ntp(p) * 16 + 4 * q, q, ro);
-        };
-        if constexpr (S && SIG) flag_signal(lds, l, 1 - (wave >> 1), lane);  // the column tile it does not compute
-        if constexpr (WAIT) flag_wait(lds, l - 1, ctp(0), tgt);
-        u32x4 xb[3][3];
-        ldx(xb[0], 0);
-        if (NI > 1 && (1 < I1 || CROSS)) {
-            if (WAIT && 1 == I1) flag_wait(lds, l - 1, 1, tgt);
-            ldx(xb[1], 1);
-        }
-        f32x4 acc = init_of(0), nxt = acc, ev = acc;
-        EpiSt es{};  // the carry's epilogue (pass 0) and the passes' (from pass 1) never overlap
-        auto carry_step = [&](int u) {
-            if constexpr (CIN) {
-                epi_micro<EPC>(u, cy.ev, es, lds + cy.o, cy.opl);
-                if (u == NSC - 1) flag_signal(lds, l - 1, cy.ct, lane);
-            }
-        };
-        auto pass_step = [&](int u, int p) {  // epilogue micro-step u of pass p (run during pass p + 1)
-            epi_micro<EPI>(u, ev, es, out_of(p), L::out_pl(l));
-            if (SIG && !S && u == NSTEP - 1 && p == T - 1) flag_signal(lds, l, 0, lane);  // column tile 0 complete
-        };
-#pragma unroll
-        for (int p = 0; p < NP; ++p) {
-            if (p + 1 < NP) nxt = init_of(p + 1);
-            if (!CROSS && p * KC == I1) {  // T = 1 after a carry: the carry is stored and signalled by now
-                if (WAIT) flag_wait(lds, l - 1, 1, tgt);
-                ldx(xb[I1 % 3], I1);
-                if (KC > 1) ldx(xb[(I1 + 1) % 3], I1 + 1);
-            }
-#pragma unroll
-            for (int kc = 0; kc < KC; ++kc) {
-                const int i = p * KC + kc;
-                if (i + 2 < NI && (CROSS || i + 2 < I1 || i >= I1)) {  // !CROSS: steps I1, I1 + 1 at pass start
-                    if (WAIT && i + 2 == I1) flag_wait(lds, l - 1, 1, tgt);
-                    ldx(xb[(i + 2) % 3], i + 2);
-                }
-#pragma unroll
-                for (int m = 0; m < 6; ++m) {
-                    acc = mm1(S ? 0 : p % T, kc, m, xb[i % 3], acc);
-                    const int u = kc * 6 + m;
-                    if (p == 0 && u < NSC) carry_step(u);
-                    if (p > 0 && u < NSTEP) pass_step(u, p - 1);
-                    if (i * 6 + m < NS) side(i * 6 + m);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            if (p == 0)
-#pragma unroll
-                for (int u = KC * 6; u < NSC; ++u) carry_step(u);  // a first pass shorter than the carried epilogue
-            if (p > 0)
-#pragma unroll
-                for (int u = KC * 6; u < NSTEP; ++u) pass_step(u, p - 1);
-            ev = acc;
-            acc = nxt;
-        }
-        if constexpr (COUT) {
-            cy.ev = ev;
-            cy.o = (int)(out_of(NP - 1) - lds);
-            cy.opl = L::out_pl(l);
-            cy.ct = ctp(NP - 1);
-        } else {
-#pragma unroll
-            for (int u = 0; u < NSTEP; ++u) epi_micro<EPI>(u, ev, es, out_of(NP - 1), L::out_pl(l));
-            if constexpr (SIG) flag_signal(lds, l, ctp(NP - 1), lane);
-        }
-#pragma unroll
-        for (int k = NI * 6; k < NS; ++k) side(k);
-    }
-
-    template <int l, int NS = 0, bool CIN = false, bool COUT = false, class SIDE>
-    static MPCD_DEV void layer_f(const WS<l> &w, SIDE side, Carry &cy, char *lds, int wave, int lane, uint32_t tgt)
-    {
-        hidden_fl<l, NS, CIN, COUT>(
-            [&](int j, int kc, int m, const u32x4 (&x)[3], f32x4 acc) { return mfma_bf(w.v[j][kc][wpl(m)], x[xpl(m)], acc); },
-            side, cy, lds, wave, lane, tgt);
-    }
-
-    template <int li, int NS = 0, bool CIN = false, bool COUT = false, class SIDE>
-    static MPCD_DEV void layer_res_f(const Res &r, const Tail &t, SIDE side, Carry &cy, char *lds, int wave, int lane,
-                                     uint32_t tgt)
-    {
-        hidden_fl<RES_L0 + li, NS, CIN, COUT>(
-            [&](int j, int kc, int m, const u32x4 (&x)[3], f32x4 acc) {
-                const int g = (li * 2 + j) * 4 + kc;
-                if (g >= RES_AG) return mfma_bf(t.v[g - RES_AG][wpl(m)], x[xpl(m)], acc);
-                const bool first = kc == 0 && m == 0;
-                const bool last = (kc == 3 || g + 1 == RES_AG) && m == 5;
-                if (first && last) return mfma_agpr1<true, true>(r.a[g][wpl(m)], x[xpl(m)], acc);
-                if (first) return mfma_agpr1<true, false>(r.a[g][wpl(m)], x[xpl(m)], acc);
-                if (last) return mfma_agpr1<false, true>(r.a[g][wpl(m)], x[xpl(m)], acc);
-                return mfma_agpr1<false, false>(r.a[g][wpl(m)], x[xpl(m)], acc);
-            },
-            side, cy, lds, wave, lane, tgt);
-    }
-
     template <int l, int NS = 0, class SIDE>
     static MPCD_DEV void layer(const WS<l> &w, SIDE side, char *lds, int wave, int lane)
     {
@@ -1012,7 +779,6 @@ struct MlpRw {
                 bic[cond_off(j) + i] = wp[woffx<D0>(2 * j + 1) + wfl<D0>(2 * j + 1) + i];
         for (int i = threadIdx.x; i < COND_TOTAL; i += RW_T) cps[i] = CTX ? p.cproj[i] : 0.f;
         if (threadIdx.x < CPW) reinterpret_cast<uint32_t *>(lds + L::AMX)[threadIdx.x] = 0u;
-        if (FLAGS && threadIdx.x < 32) reinterpret_cast<uint32_t *>(lds + CNT)[threadIdx.x] = 0u;  // (before the 1st bar)
         uint32_t am[2] = {0u, 0u};
         for (int i = threadIdx.x; i < CPW * QUADS; i += RW_T) {  // x_T (fp32 + planes)
             const int c = i / QUADS, qd = i - c * QUADS;
@@ -1050,19 +816,12 @@ struct MlpRw {
             tacc[2 * bk + 1] += tprev - t;
             bk = bk == 13 ? 0 : bk + 1;
         };
-        auto mark = [&] {  // a counter-synchronised layer boundary (FLAGS): the segment's cycles, no wait column
-            const uint64_t t = __builtin_readcyclecounter();
-            tacc[2 * bk] += t - tprev;
-            tprev = t;
-            bk = bk == 13 ? 0 : bk + 1;
-        };
 #else
 #if MPCD_RW_EXP_BAR2
         auto bar = [] { lds_barrier(); lds_barrier(); };  // timing experiment: the cost of one more barrier per layer
 #else
         auto bar = [] { lds_barrier(); };
 #endif
-        auto mark = [] {};
 #endif
 
         for (int s = 0; s < p.n_steps; ++s) {
@@ -1125,84 +884,41 @@ struct MlpRw {
 #endif
                 }
             };
-            if constexpr (FLAGS) {
-                // layers 1..12 synchronised by the per-column-tile counters (hidden_fl), the N >= 64 layers passing
-                // their last epilogue on as a carry
-                Carry cy;
-                const uint32_t tgt = 4u * (uint32_t)(s + 1);
-                layer_f<1, NFRAG<4>>(w1, [&](int k) { load_ws1<4>(w4, ws, wave, lane16, k); }, cy, lds, wave, lane, tgt);
-                mark();
-                layer_f<2, 0, false, CARRY>(w2, none, cy, lds, wave, lane, tgt);
-                mark();
-                layer_f<3, 0, CARRY, CARRY>(w3, none, cy, lds, wave, lane, tgt);
-                mark();
-                layer_f<4, 0, CARRY, CARRY>(w4, none, cy, lds, wave, lane, tgt);
-                mark();
-                layer_res_f<0, 0, CARRY, CARRY>(res, tail, none, cy, lds, wave, lane, tgt);
-                mark();
-                layer_res_f<1, NFRAG<8>, CARRY, CARRY>(res, tail, [&](int k) { load_ws1<8>(w8, ws, wave, lane16, k); }, cy,
-                                                     lds, wave, lane, tgt);
-                load_tail(tail, ws, wave, lane16);
-                mark();
-                layer_res_f<2, 0, CARRY, CARRY>(res, tail, none, cy, lds, wave, lane, tgt);
-                load_ws<9>(w9, ws, wave, lane16);
-                mark();
-                if (s + 1 < p.n_steps) sp = load_plan(p.plan, s + 1);
-                if constexpr (STAGED_NOISE) {
-                    ph_init(ph, p, s + 2, cand0, wave, lane);  // step s + 1's noise is Philox slice s + 2 (fetch_noise)
-                    layer_f<8, NPH, CARRY, CARRY>(w8, [&](int k) { ph_step(ph, k); }, cy, lds, wave, lane, tgt);
-                } else {
-                    layer_f<8, 0, true, true>(w8, none, cy, lds, wave, lane, tgt);
-                }
-                load_ws<10>(w10, ws, wave, lane16);  // after L8: w8's 96 registers are free again
-                mark();
-                layer_f<9, NFRAG<11> + NFRAG<12> + NFRAG<13>, true, false>(w9, side9, cy, lds, wave, lane, tgt);
-                mark();
-                layer_f<10>(w10, none, cy, lds, wave, lane, tgt);
-                noise_next();
-                load_ws<0>(w0, ws, wave, lane16);  // next step's layer 0 (unconditional: path-independent load count)
-                mark();
-                layer_f<11>(w11, none, cy, lds, wave, lane, tgt);
-                mark();
-                layer_f<12>(w12, none, cy, lds, wave, lane, tgt);
-                bar();
+            layer<1, NFRAG<4>>(w1, [&](int k) { load_ws1<4>(w4, ws, wave, lane16, k); }, lds, wave, lane);
+            bar();
+            layer<2>(w2, none, lds, wave, lane);
+            bar();
+            layer<3>(w3, none, lds, wave, lane);
+            bar();
+            layer<4>(w4, none, lds, wave, lane);
+            bar();
+            layer_res<0>(res, tail, none, lds, wave, lane);
+            bar();
+            layer_res<1, NFRAG<8>>(res, tail, [&](int k) { load_ws1<8>(w8, ws, wave, lane16, k); }, lds, wave, lane);
+            load_tail(tail, ws, wave, lane16);
+            bar();
+            layer_res<2>(res, tail, none, lds, wave, lane);
+            load_ws<9>(w9, ws, wave, lane16);
+            bar();
+            if (s + 1 < p.n_steps) sp = load_plan(p.plan, s + 1);
+            if constexpr (STAGED_NOISE) {
+                ph_init(ph, p, s + 2, cand0, wave, lane);  // step s + 1's noise is Philox slice s + 2 (fetch_noise)
+                layer<8, NPH>(w8, [&](int k) { ph_step(ph, k); }, lds, wave, lane);
             } else {
-                layer<1, NFRAG<4>>(w1, [&](int k) { load_ws1<4>(w4, ws, wave, lane16, k); }, lds, wave, lane);
-                bar();
-                layer<2>(w2, none, lds, wave, lane);
-                bar();
-                layer<3>(w3, none, lds, wave, lane);
-                bar();
-                layer<4>(w4, none, lds, wave, lane);
-                bar();
-                layer_res<0>(res, tail, none, lds, wave, lane);
-                bar();
-                layer_res<1, NFRAG<8>>(res, tail, [&](int k) { load_ws1<8>(w8, ws, wave, lane16, k); }, lds, wave, lane);
-                load_tail(tail, ws, wave, lane16);
-                bar();
-                layer_res<2>(res, tail, none, lds, wave, lane);
-                load_ws<9>(w9, ws, wave, lane16);
-                bar();
-                if (s + 1 < p.n_steps) sp = load_plan(p.plan, s + 1);
-                if constexpr (STAGED_NOISE) {
-                    ph_init(ph, p, s + 2, cand0, wave, lane);  // step s + 1's noise is Philox slice s + 2 (fetch_noise)
-                    layer<8, NPH>(w8, [&](int k) { ph_step(ph, k); }, lds, wave, lane);
-                } else {
-                    layer<8>(w8, none, lds, wave, lane);
-                }
-                load_ws<10>(w10, ws, wave, lane16);  // after L8: w8's 96 registers are free again
-                bar();
-                layer<9, NFRAG<11> + NFRAG<12> + NFRAG<13>>(w9, side9, lds, wave, lane);
-                bar();
-                layer<10>(w10, none, lds, wave, lane);
-                noise_next();
-                load_ws<0>(w0, ws, wave, lane16);  // next step's layer 0 (unconditional: path-independent load count)
-                bar();
-                layer<11>(w11, none, lds, wave, lane);
-                bar();
-                layer<12>(w12, none, lds, wave, lane);
-                bar();
+                layer<8>(w8, none, lds, wave, lane);
             }
+            load_ws<10>(w10, ws, wave, lane16);  // after L8: w8's 96 registers are free again
+            bar();
+            layer<9, NFRAG<11> + NFRAG<12> + NFRAG<13>>(w9, side9, lds, wave, lane);
+            bar();
+            layer<10>(w10, none, lds, wave, lane);
+            noise_next();
+            load_ws<0>(w0, ws, wave, lane16);  // next step's layer 0 (unconditional: path-independent load count)
+            bar();
+            layer<11>(w11, none, lds, wave, lane);
+            bar();
+            layer<12>(w12, none, lds, wave, lane);
+            bar();
 #ifdef MPCD_PROF_LAYERS
             final_and_update(w13, lds, p, cur, s, cand0, nzc, am, wave, lane, tacc);  // "-" row: MFMAs / update
 #else
@@ -1243,13 +959,11 @@ __global__ __launch_bounds__(RW_T, 1) void mlp_rw_kernel(const MlpSampleArgs p)
 template <int D0, int SMODE, bool CTX, int R>
 hipError_t launch_rw_r(const MlpSampleArgs &a, hipStream_t stream)
 {
-    using K = MlpRw<D0, SMODE, CTX, R>;
-    using L = typename K::L;
-    static_assert(K::LDS_BYTES <= 160 * 1024, "LDS budget (160 KiB per CU)");
+    using L = Lds3<D0, MlpRw<D0, SMODE, CTX, R>::NB, R>;
+    static_assert(L::total <= 160 * 1024, "LDS budget (160 KiB per CU)");
     if (hipError_t e = allow_max_lds<&mlp_rw_kernel<D0, SMODE, CTX, R>>(); e != hipSuccess) return e;
     const int64_t blocks = (a.batch + L::CPW - 1) / L::CPW;
-    hipLaunchKernelGGL((mlp_rw_kernel<D0, SMODE, CTX, R>), dim3((unsigned)blocks), dim3(RW_T), (size_t)K::LDS_BYTES, stream,
-                       a);
+    hipLaunchKernelGGL((mlp_rw_kernel<D0, SMODE, CTX, R>), dim3((unsigned)blocks), dim3(RW_T), (size_t)L::total, stream, a);
     return hipGetLastError();
 }
 

@@ -3,8 +3,10 @@
 bench.py's step is `plan.mpc_step(x0, double_int2d, B, w=0.01, seed=...)` with in-kernel Philox noise, the
 default (auto) MLP workgroup layout, the native one-call step (mpcd_mpc_step: sampler, chain-wide clip flag,
 fp64 rollout/cost fused with the argmin, winner row). Here that same call runs at BASELINE cfg 2 (B=4096,
-H=32, N=100: the resident-weight 32-row `mlp_rw_kernel<64, DDPM_CFG, ctx, 32>`) and cfg 1 (B=64, H=16, N=50:
-its 16-row form, mlp_rw_kernel<32, DDPM_CFG, ctx, 16>); every candidate's Philox draws are replayed (mpcd_philox_noise) through the oracle
+H=32, N=100) and cfg 1 (B=64, H=16, N=50) for both MLP numerics: f32x3, the bench default (the resident-weight
+split-bf16 `mlp_rw_kernel<64, DDPM_CFG, ctx, 32>` at cfg 2, its 16-row form `mlp_rw_kernel<32, DDPM_CFG, ctx, 16>`
+at cfg 1) and f16x2 (`mlp_h2_kernel<64, DDPM_CFG, ctx, 32>` / `<32, DDPM_CFG, ctx, 16>`, --dtype f16x2); every
+candidate's Philox draws are replayed (mpcd_philox_noise) through the oracle
 sampler (diffusion_model_base.py:181-209, sample_functions.py:17-44), the oracle LimitsNormalizer's
 chain-wide clip rule (normalization.py:156-167) and the C cost oracle, then argmin
 (scripts/inference/inference_(mpd).py:335-338). Bars: samples per trajectory 1e-4 and
@@ -31,8 +33,9 @@ CASES = {"cfg1": (64, 16, 2, 4, 50), "cfg2": (4096, 32, 2, 4, 100)}
 @pytest.mark.parametrize("dtype", ["f32x3", "f16x2"])
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_timed_mpc_step_matches_oracle_full_batch(name, dtype):
-    """Both fp32-class numerics of the MLP: the split-bf16 kernels (f32x3) and the two-term fp16 kernel (f16x2,
-    csrc/mlp_h2.hip: mlp_h2_kernel<64, DDPM_CFG, ctx, 32> at cfg2, <32, DDPM_CFG, ctx, 16> at cfg1)."""
+    """Both MLP numerics: the fp32-accurate split-bf16 kernels (f32x3, the bench default) and the two-term fp16 kernel
+    (f16x2: 22-bit operands, fp16 range; csrc/mlp_h2.hip: mlp_h2_kernel<64, DDPM_CFG, ctx, 32> at cfg2,
+    <32, DDPM_CFG, ctx, 16> at cfg1), each against the same oracle bars."""
     B, H, d, C, N = CASES[name]
     torch.set_num_threads(min(16, torch.get_num_threads()))
     net = make_mlp(d, H, C, seed=0)
