@@ -84,6 +84,15 @@ MPCD_DEV f32x4 mfma_agpr1(const u32x4 &w, const u32x4 &x, f32x4 acc)
 #ifndef MPCD_RW_ILV
 #define MPCD_RW_ILV 1
 #endif
+// MPCD_RW_PF: k-chunks of operand fragments read ahead of the MFMAs in hidden_ilv (2: a ring of three)
+#ifndef MPCD_RW_PF
+#define MPCD_RW_PF 2
+#endif
+// MPCD_RW_TABLE_EARLY = 1: the next step's cond tables (TPC / TPU) are written after Linear 11 (the last layer that
+// reads them) instead of at the step's start, where their LDS round trip delayed Linear 0's first operand reads
+#ifndef MPCD_RW_TABLE_EARLY
+#define MPCD_RW_TABLE_EARLY 0
+#endif
 // MPCD_RW_EPI_STEPS = 1: the epilogue spread as 1-2 VALU ops per MFMA slot (hidden_ilv); 0: five units
 #ifndef MPCD_RW_EPI_STEPS
 #define MPCD_RW_EPI_STEPS 1
@@ -353,9 +362,12 @@ struct MlpRw {
             *reinterpret_cast<u32x2 *>(o + L::out_pl(l)) = p1;
             *reinterpret_cast<u32x2 *>(o + 2 * L::out_pl(l)) = p2;
         };
-        u32x4 xb[3][3];
-        ldx(xb[0], 0);
-        if (NI > 1) ldx(xb[1], 1);
+        // operand fragments read PF k-chunks ahead (a ring of PF + 1)
+        constexpr int PF = MPCD_RW_PF;
+        u32x4 xb[PF + 1][3];
+#pragma unroll
+        for (int i = 0; i < PF; ++i)
+            if (i < NI) ldx(xb[i], i);
         f32x4 acc = init_of(0), nxt = acc, ev = acc;
 #if MPCD_RW_EPI_STEPS
         // The previous pass's epilogue as NSTEP micro-steps of one or two VALU instructions, one after each MFMA:
@@ -402,10 +414,10 @@ struct MlpRw {
 #pragma unroll
             for (int kc = 0; kc < KC; ++kc) {
                 const int i = p * KC + kc;
-                if (i + 2 < NI) ldx(xb[(i + 2) % 3], i + 2);
+                if (i + PF < NI) ldx(xb[(i + PF) % (PF + 1)], i + PF);
 #pragma unroll
                 for (int m = 0; m < 6; ++m) {
-                    acc = mm1(jp(p), kc, m, xb[i % 3], acc);
+                    acc = mm1(jp(p), kc, m, xb[i % (PF + 1)], acc);
                     const int u = kc * 6 + m;
                     if (p > 0 && u < NSTEP) epi_step(u, p - 1);
                     if (i * 6 + m < NS) side(i * 6 + m);
@@ -432,10 +444,10 @@ struct MlpRw {
 #pragma unroll
             for (int kc = 0; kc < KC; ++kc) {
                 const int i = p * KC + kc;
-                if (i + 2 < NI) ldx(xb[(i + 2) % 3], i + 2);
+                if (i + PF < NI) ldx(xb[(i + PF) % (PF + 1)], i + PF);
 #pragma unroll
                 for (int m = 0; m < 6; ++m) {
-                    acc = mm1(jp(p), kc, m, xb[i % 3], acc);
+                    acc = mm1(jp(p), kc, m, xb[i % (PF + 1)], acc);
                     const int u = kc * 6 + m;
                     if (p > 0 && u < 5) epi_unit(u, ev, p - 1);
                     else if (i * 6 + m - 5 * p < NS) side(i * 6 + m - 5 * p);  // the k-th free slot
@@ -839,14 +851,19 @@ struct MlpRw {
             load_ws<2>(w2, ws, wave, lane16);
             bar();
             // this step's time projections + cond biases (+ shared context part) -> TPU / TPC: one f32x4 per thread
-            if (threadIdx.x < COND_TOTAL / 2) {
-                const bool ctx_half = threadIdx.x >= COND_TOTAL / 4;
-                const int k = ctx_half ? (int)threadIdx.x - COND_TOTAL / 4 : (int)threadIdx.x;
-                f32x4 u = tpre + reinterpret_cast<const f32x4 *>(lds + L::BIC)[k];
-                if (ctx_half) u = u + reinterpret_cast<const f32x4 *>(lds + L::CPS)[k];
-                reinterpret_cast<f32x4 *>(lds + (ctx_half ? L::TPC : L::TPU))[k] = u;
+            auto table = [&] {
+                if (threadIdx.x < COND_TOTAL / 2) {
+                    const bool ctx_half = threadIdx.x >= COND_TOTAL / 4;
+                    const int k = ctx_half ? (int)threadIdx.x - COND_TOTAL / 4 : (int)threadIdx.x;
+                    f32x4 u = tpre + reinterpret_cast<const f32x4 *>(lds + L::BIC)[k];
+                    if (ctx_half) u = u + reinterpret_cast<const f32x4 *>(lds + L::CPS)[k];
+                    reinterpret_cast<f32x4 *>(lds + (ctx_half ? L::TPC : L::TPU))[k] = u;
+                }
+            };
+            if (!MPCD_RW_TABLE_EARLY || s == 0) {
+                table();
+                tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 1 < p.n_steps ? s + 1 : s) * COND_TOTAL)[tpi];
             }
-            tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 1 < p.n_steps ? s + 1 : s) * COND_TOTAL)[tpi];
             WS<3> w3;
             layer<0, NFRAG<3>>(w0, [&](int k) { load_ws1<3>(w3, ws, wave, lane16, k); }, lds, wave, lane);
             bar();
@@ -917,6 +934,10 @@ struct MlpRw {
             bar();
             layer<11>(w11, none, lds, wave, lane);
             bar();
+            if (MPCD_RW_TABLE_EARLY && s + 1 < p.n_steps) {  // step s + 1's tables (Linear 11 read step s's last)
+                table();
+                tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 2 < p.n_steps ? s + 2 : s + 1) * COND_TOTAL)[tpi];
+            }
             layer<12>(w12, none, lds, wave, lane);
             bar();
 #ifdef MPCD_PROF_LAYERS
