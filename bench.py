@@ -59,7 +59,8 @@ PEAK_FP32 = 157.3e12      # MI355X dense fp32 MFMA / vector peak, FLOP/s (MI355X
 PEAK_BF16 = 2516.6e12     # MI355X dense bf16 / fp16 MFMA peak: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz
 LIB = os.path.join(ROOT, "mpc_via_diffusion_model_amd", "libmpcd.so")
 PMC_FILES = {("cfg2", "f32"): os.path.join(ROOT, "profiles", "r1_pmc_mlp_sampler.json"),
-             ("cfg2", "f32x3"): os.path.join(ROOT, "profiles", "r4_pmc_mlp_rw.json"),
+             ("cfg2", "f32x3"): os.path.join(ROOT, "profiles", "r6_pmc_cfg2_mlp_rw.json"),
+             ("cfg1", "f32x3"): os.path.join(ROOT, "profiles", "r6_pmc_cfg1_mlp_rw.json"),
              ("cfg2", "f16x2"): os.path.join(ROOT, "profiles", "r5_pmc_mlp_h2.json"),
              # U-Net: HBM bytes of one noise-net forward (the fused launch of one denoise step, PMC FETCH_SIZE x2 +
              # WRITE_SIZE, tools/unet_roofline.py) at B

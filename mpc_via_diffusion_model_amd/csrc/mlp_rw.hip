@@ -91,7 +91,12 @@ MPCD_DEV f32x4 mfma_agpr1(const u32x4 &w, const u32x4 &x, f32x4 acc)
 // MPCD_RW_TABLE_EARLY = 1: the next step's cond tables (TPC / TPU) are written after Linear 11 (the last layer that
 // reads them) instead of at the step's start, where their LDS round trip delayed Linear 0's first operand reads
 #ifndef MPCD_RW_TABLE_EARLY
-#define MPCD_RW_TABLE_EARLY 0
+#define MPCD_RW_TABLE_EARLY 1
+#endif
+// MPCD_RW_W8_SPLIT = 1: Linear 8's streamed fragments issued half in Linear 5's MFMA slots, half in Linear 6's
+// (0: all 24 in Linear 6's)
+#ifndef MPCD_RW_W8_SPLIT
+#define MPCD_RW_W8_SPLIT 0
 #endif
 // MPCD_RW_EPI_STEPS = 1: the epilogue spread as 1-2 VALU ops per MFMA slot (hidden_ilv); 0: five units
 #ifndef MPCD_RW_EPI_STEPS
@@ -909,9 +914,11 @@ struct MlpRw {
             bar();
             layer<4>(w4, none, lds, wave, lane);
             bar();
-            layer_res<0>(res, tail, none, lds, wave, lane);
+            constexpr int W8A = MPCD_RW_W8_SPLIT ? NFRAG<8> / 2 : 0;  // Linear 8 fragments issued during Linear 5
+            layer_res<0, W8A>(res, tail, [&](int k) { load_ws1<8>(w8, ws, wave, lane16, k); }, lds, wave, lane);
             bar();
-            layer_res<1, NFRAG<8>>(res, tail, [&](int k) { load_ws1<8>(w8, ws, wave, lane16, k); }, lds, wave, lane);
+            layer_res<1, NFRAG<8> - W8A>(res, tail, [&](int k) { load_ws1<8>(w8, ws, wave, lane16, W8A + k); }, lds, wave,
+                                         lane);
             load_tail(tail, ws, wave, lane16);
             bar();
             layer_res<2>(res, tail, none, lds, wave, lane);

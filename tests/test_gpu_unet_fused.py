@@ -7,6 +7,7 @@ Downsample1d / Upsample1d (layers.py:258-355), p_mean_variance_CFG + ddpm_cart_p
 Bars: f32x3 and f16x2 (two-term fp16, the fused program's P = 2) eps 2e-5 of |eps| max, chains at the SURVEY §8d
 bar (1e-4 per trajectory and elementwise); f16 (BASELINE cfg 5's fp16 operands) reported, bounded at 2e-2 eps / 5e-2
 trajectory."""
+import numpy as np
 import pytest
 import torch
 
@@ -172,3 +173,33 @@ def test_fused_forced_on_uncovered_net_raises():
     finally:
         force_unet_path("auto")
     assert torch.isfinite(plan.sample_trajectories(torch.zeros(1, 3), 4, 64)).all()
+
+
+def test_f16x2_out_of_range_reruns_in_f32x3():
+    """The fused U-Net's two-term fp16 program (P = 2) computes in the fp16 range. Every ResidualTemporalBlock's
+    cond projection x 1e6 puts the conv inputs after it far above 65,504 (GroupNorm comes before that add): the
+    P = 2 chain comes back with a NaN, the planner re-runs the call with the net's split-bf16 program (mpcd_force_f32x3)
+    and returns exactly what an f32x3 plan of the same weights returns; mpcd_mpc_step does the same by itself."""
+    from mpc_via_diffusion_model_amd import _native as N_
+    from mpc_via_diffusion_model_amd import systems
+    d, H, C, B, N = 1, 32, 5, 16, 25
+    net = make_unet(d, C, seed=3)
+    with torch.no_grad():
+        for m in net.modules():
+            if isinstance(m, torch.nn.Sequential) and len(m) >= 2 and isinstance(m[1], torch.nn.Linear) and \
+                    isinstance(m[0], torch.nn.Mish):
+                m[1].weight.mul_(1e6)
+    p16 = DiffusionMPC(NetSpec("unet", d, H, C, dtype="f16x2"), net.state_dict(), n_diffusion_steps=N)
+    p32 = DiffusionMPC(NetSpec("unet", d, H, C, dtype="f32x3"), net.state_dict(), n_diffusion_steps=N)
+    assert p16.unet_form()["planes"] == 2 and p16.unet_form()["fused"]
+    ctx = torch.rand(1, C, generator=torch.Generator().manual_seed(1)) * 2 - 1
+    a = p16.sample_trajectories(ctx, B, H, seed=3)
+    assert p16.last_f32x3_rerun, "the two-term fp16 program should have left the fp16 range here"
+    b = p32.sample_trajectories(ctx, B, H, seed=3)
+    torch.cuda.synchronize()
+    assert torch.isfinite(a).all() and torch.equal(a, b)
+    x0 = np.random.default_rng(2).uniform(-1, 1, C)
+    r = p16.mpc_step(x0, systems.get("cartpole_nl5"), B, w=0.01, seed=5)
+    r_ref = p32.mpc_step(x0, systems.get("cartpole_nl5"), B, w=0.01, seed=5)
+    assert r.flags & N_.MPCD_STEP_F32X3_RERUN
+    assert r.best_index == r_ref.best_index and r.best_cost == r_ref.best_cost and torch.equal(r.u_norm, r_ref.u_norm)
