@@ -93,10 +93,21 @@ MPCD_DEV f32x4 mfma_agpr1(const u32x4 &w, const u32x4 &x, f32x4 acc)
 #ifndef MPCD_RW_TABLE_EARLY
 #define MPCD_RW_TABLE_EARLY 1
 #endif
-// MPCD_RW_W8_SPLIT = 1: Linear 8's streamed fragments issued half in Linear 5's MFMA slots, half in Linear 6's
-// (0: all 24 in Linear 6's)
+// MPCD_RW_W8_SPLIT = 1 (default): Linear 8's streamed fragments issued half in Linear 5's MFMA slots, half in
+// Linear 6's (0: all 24 in Linear 6's; profiles/r6_mlp_tuning_ab.txt)
 #ifndef MPCD_RW_W8_SPLIT
-#define MPCD_RW_W8_SPLIT 0
+#define MPCD_RW_W8_SPLIT 1
+#endif
+// MPCD_RW_TABLE_SIDE = 1 (default, with TABLE_EARLY): the table's two reads and its write ride in Linear 12's
+// MFMA slots
+#ifndef MPCD_RW_TABLE_SIDE
+#define MPCD_RW_TABLE_SIDE 1
+#endif
+// MPCD_RW_XREG = 1 (default): each lane keeps its x_t quads in registers across steps (the fp32 copy in LDS goes),
+// and the update's x-only products (a x, c2 x, std z) are formed while the final layer's operand reads are in
+// flight. Together with TABLE_SIDE: kernel 1.098 -> 1.090 ms at cfg2 (profiles/r6_mlp_tuning_ab.txt, 3 repeats)
+#ifndef MPCD_RW_XREG
+#define MPCD_RW_XREG 1
 #endif
 // MPCD_RW_EPI_STEPS = 1: the epilogue spread as 1-2 VALU ops per MFMA slot (hidden_ilv); 0: five units
 #ifndef MPCD_RW_EPI_STEPS
@@ -531,9 +542,10 @@ struct MlpRw {
         p2 = u32x2{pk_bf16(r0, r1), pk_bf16(r2, r3)};
     }
 
+    template <bool FP32 = true>
     static MPCD_DEV void store_x(char *lds, int cl, int n, const f32x4 &x)
     {
-        *reinterpret_cast<f32x4 *>(lds + L::XB + (cl * L::SX + n) * 4) = x;
+        if (FP32) *reinterpret_cast<f32x4 *>(lds + L::XB + (cl * L::SX + n) * 4) = x;
         u32x2 p0, p1, p2;
         split3s(x, p0, p1, p2);
         char *o = lds + L::S1 + cl * L::RS + ((n * 2) ^ (swz(cl) << 4));
@@ -561,9 +573,28 @@ struct MlpRw {
 #define MPCD_FINAL_PROF
 #define MPCD_FINAL_MARK(k, dep)
 #endif
+    // x_t of the update's (n-tile j, column group g) quads, when MPCD_RW_XREG keeps it in registers
+    static constexpr int XG = NB == 2 ? 1 : NCT;
+    static MPCD_DEV bool x_lane(int j, int wave, int col)
+    {
+        return (D0 / 16 % 4 == 0 || wave + 4 * j < D0 / 16) && !(R == 16 && NB == 2 && col >= 8);
+    }
+    static MPCD_DEV void load_xr(f32x4 (&xr)[NZT][XG], const char *lds, int wave, int lane)
+    {
+        const int col = lane & 15, q = lane >> 4;
+#pragma unroll
+        for (int j = 0; j < NZT; ++j)
+#pragma unroll
+            for (int g = 0; g < XG; ++g) {
+                const int cl = NB == 2 ? col : g * 16 + col, n = (wave + 4 * j) * 16 + 4 * q;
+                xr[j][g] = x_lane(j, wave, col) ? *reinterpret_cast<const f32x4 *>(lds + L::XB + (cl * L::SX + n) * 4)
+                                                : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+    }
+
     static MPCD_DEV void final_and_update(const FW &f, char *lds, const MlpSampleArgs &p, const StepPlan &sp, int s,
-                                          int64_t cand0, const f32x4 (&nz)[NZT][NB], uint32_t (&am)[2], int wave,
-                                          int lane MPCD_FINAL_PROF)
+                                          int64_t cand0, const f32x4 (&nz)[NZT][NB], uint32_t (&am)[2],
+                                          f32x4 (&xr)[NZT][XG], int wave, int lane MPCD_FINAL_PROF)
     {
 #ifdef MPCD_PROF_LAYERS
         uint64_t tmark = __builtin_readcyclecounter();
@@ -581,6 +612,27 @@ struct MlpRw {
         u32x4 xf[NCT][3];
 #pragma unroll
         for (int c = 0; c < NCT; ++c) load_x3(xf[c], lds + L::T1 + (c * 16 + col) * L::RS + 16 * (q ^ swz(col)), L::PL);
+        // MPCD_RW_XREG, DDPM: the x-only products of the update under the operand reads' latency (each through a
+        // fence, the same values as in the update's order: a x, c2 x, std z are separate roundings there too)
+        constexpr bool PRE = MPCD_RW_XREG && IS_DDPM;
+        f32x4 pax[T][XG], pcx[T][XG], psz[T][XG];
+        if constexpr (PRE) {
+            auto fn = [](float &v) { asm volatile("" : "+v"(v)); };
+#pragma unroll
+            for (int j = 0; j < T; ++j)
+#pragma unroll
+                for (int g = 0; g < XG; ++g)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float xv = xr[j][g][r];
+                        float a = sp.a * xv, c = sp.c2 * xv, z = sp.std * nz[j][0][r];
+                        fn(a); fn(c); fn(z);
+                        pax[j][g][r] = a;
+                        pcx[j][g][r] = c;
+                        psz[j][g][r] = z;
+                        am[g] = max(am[g], abs_bits(xv));
+                    }
+        }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int c = 0; c < NCT; ++c)
@@ -625,12 +677,27 @@ struct MlpRw {
                     }
                     continue;
                 }
-                const f32x4 x = *reinterpret_cast<const f32x4 *>(lds + L::XB + (cl * L::SX + n) * 4);
+                const f32x4 x = MPCD_RW_XREG ? xr[j][g] : *reinterpret_cast<const f32x4 *>(lds + L::XB + (cl * L::SX + n) * 4);
                 f32x4 xn;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float xv = x[r];
                     float o;
+                    if constexpr (PRE) {
+                        auto fn = [](float &v) { asm volatile("" : "+v"(v)); };
+                        float x0c = pax[j][g][r] - sp.b * ec[r];
+                        fn(x0c);
+                        float x0u = pax[j][g][r] - sp.b * eu[r];
+                        fn(x0u);
+                        float x0 = p.wp1 * x0c - p.wf * x0u;
+                        x0 = clamp1(x0);
+                        float mean = sp.c1 * x0 + pcx[j][g][r];
+                        fn(mean);
+                        o = (sp.flags & PLAN_NOISE) ? mean + psz[j][g][r] : mean;
+                        xn[r] = o;
+                        am[g] = max(am[g], abs_bits(o));
+                        continue;
+                    }
                     if (IS_DDPM) {
                         // every intermediate through a fence: the SLP vectorizer paired the four values' products
                         // into v_pk_mul / v_pk_add_f32, dearer than the plain ops here (same values either way)
@@ -657,7 +724,8 @@ struct MlpRw {
                     xn[r] = o;
                     am[g] = max(am[g], max(abs_bits(xv), abs_bits(o)));
                 }
-                store_x(lds, cl, n, xn);
+                store_x<!MPCD_RW_XREG>(lds, cl, n, xn);
+                if (MPCD_RW_XREG) xr[j][g] = xn;
                 if (gc < p.batch) {
                     if (p.chain) *reinterpret_cast<f32x4 *>(p.chain + ((size_t)(s + 1) * p.batch + gc) * D0 + n) = xn;
                     if (last) *reinterpret_cast<f32x4 *>(p.x_out + (size_t)gc * D0 + n) = xn;
@@ -808,6 +876,11 @@ struct MlpRw {
             }
             store_x(lds, c, qd * 4, z);
         }
+        f32x4 xr[NZT][XG];
+        if constexpr (MPCD_RW_XREG) {
+            lds_barrier();
+            load_xr(xr, lds, wave, lane);
+        }
 
         int wofs = 0;
         WS<0> w0;
@@ -941,16 +1014,36 @@ struct MlpRw {
             bar();
             layer<11>(w11, none, lds, wave, lane);
             bar();
-            if (MPCD_RW_TABLE_EARLY && s + 1 < p.n_steps) {  // step s + 1's tables (Linear 11 read step s's last)
-                table();
-                tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 2 < p.n_steps ? s + 2 : s + 1) * COND_TOTAL)[tpi];
+            if constexpr (MPCD_RW_TABLE_EARLY && MPCD_RW_TABLE_SIDE) {
+                // step s + 1's tables as Linear 12's side work: both reads in its first MFMA slot, the add and the
+                // write in its last (Linear 11 read step s's tables last; the barrier above orders them)
+                constexpr int NS12 = TL<12> * CL<12> * (A::K[12] / 32) * 6;
+                const bool ctx_half = threadIdx.x >= COND_TOTAL / 4;
+                f32x4 tb0, tb1;
+                layer<12, NS12>(w12, [&](int k) {
+                    if (k == 0) {
+                        tb0 = reinterpret_cast<const f32x4 *>(lds + L::BIC)[tpi];
+                        tb1 = reinterpret_cast<const f32x4 *>(lds + L::CPS)[tpi];
+                    } else if (k == NS12 - 1 && s + 1 < p.n_steps && threadIdx.x < COND_TOTAL / 2) {
+                        f32x4 u = tpre + tb0;
+                        if (ctx_half) u = u + tb1;
+                        reinterpret_cast<f32x4 *>(lds + (ctx_half ? L::TPC : L::TPU))[tpi] = u;
+                    }
+                }, lds, wave, lane);
+                if (s + 1 < p.n_steps)
+                    tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 2 < p.n_steps ? s + 2 : s + 1) * COND_TOTAL)[tpi];
+            } else {
+                if (MPCD_RW_TABLE_EARLY && s + 1 < p.n_steps) {  // step s + 1's tables (Linear 11 read step s's last)
+                    table();
+                    tpre = reinterpret_cast<const f32x4 *>(p.tproj + (size_t)(s + 2 < p.n_steps ? s + 2 : s + 1) * COND_TOTAL)[tpi];
+                }
+                layer<12>(w12, none, lds, wave, lane);
             }
-            layer<12>(w12, none, lds, wave, lane);
             bar();
 #ifdef MPCD_PROF_LAYERS
-            final_and_update(w13, lds, p, cur, s, cand0, nzc, am, wave, lane, tacc);  // "-" row: MFMAs / update
+            final_and_update(w13, lds, p, cur, s, cand0, nzc, am, xr, wave, lane, tacc);  // "-" row: MFMAs / update
 #else
-            final_and_update(w13, lds, p, cur, s, cand0, nzc, am, wave, lane);
+            final_and_update(w13, lds, p, cur, s, cand0, nzc, am, xr, wave, lane);
 #endif
         }
 #ifdef MPCD_PROF_LAYERS
