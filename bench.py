@@ -64,10 +64,10 @@ PMC_FILES = {("cfg2", "f32"): os.path.join(ROOT, "profiles", "r1_pmc_mlp_sampler
              ("cfg2", "f16x2"): os.path.join(ROOT, "profiles", "r5_pmc_mlp_h2.json"),
              # U-Net: HBM bytes of one noise-net forward (the fused launch of one denoise step, PMC FETCH_SIZE x2 +
              # WRITE_SIZE, tools/unet_roofline.py) at B
-             ("cfg3", "f32x3"): os.path.join(ROOT, "profiles", "r4_unet_roofline_cfg3.json"),
-             ("cfg4", "f32x3"): os.path.join(ROOT, "profiles", "r4_unet_roofline_cfg4.json"),
+             ("cfg3", "f32x3"): os.path.join(ROOT, "profiles", "r6_unet_roofline_cfg3.json"),
+             ("cfg4", "f32x3"): os.path.join(ROOT, "profiles", "r6_unet_roofline_cfg4.json"),
              ("cfg4", "f16x2"): os.path.join(ROOT, "profiles", "r5_unet_roofline_cfg4_h2.json"),
-             ("cfg5", "f16"): os.path.join(ROOT, "profiles", "r3_unet_roofline_cfg5.json")}
+             ("cfg5", "f16"): os.path.join(ROOT, "profiles", "r6_unet_roofline_cfg5.json")}
 
 
 def lib_sha256(path=None):

@@ -89,6 +89,8 @@ run_job() {
       local c=${arg:-cfg5} i=0 ctr
       local a="${UARGS[$c]} --steps 1 --reps 1 $UNET_ARGS" n=${arg:-cfg5}$UPMC_TAG
       export MPCD_UNET_TUNE_CACHE=gpurun_out/uroof/${n}_tune.txt
+      # the library the passes measure (tools/unet_roofline.py records it; bench.py compares it with the one it loads)
+      sha256sum mpc_via_diffusion_model_amd/libmpcd.so | cut -d' ' -f1 > "gpurun_out/uroof/${n}_lib.sha256"
       rm -f "$MPCD_UNET_TUNE_CACHE"
       timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d "gpurun_out/uroof/${n}_trace" -o run -f csv -- \
         python3 tools/unet_perf.py $a > "gpurun_out/uroof/${n}_trace.log" 2>&1 || return $?

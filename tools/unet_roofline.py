@@ -91,7 +91,12 @@ def main(cfg, B, H, d, C, dtype, out=None):
                       "mfma_gflop": round(fl / 1e9, 1), "mfma_frac": round(fl / dur[j] / PEAK_BF16, 3),
                       "hbm_MB": round(hbm[j] / 1e6, 1),
                       "GB_s": round(hbm[j] / dur[j] / 1e9, 1), "hbm_frac": round(hbm[j] / dur[j] / PEAK_HBM, 3),
-                      "mfma_busy": round(busy[j], 3), "mfma_insts": ctr[j].get("SQ_INSTS_MFMA", 0)})
+                      "mfma_busy": round(busy[j], 3), "mfma_insts": ctr[j].get("SQ_INSTS_MFMA", 0),
+                      # issue: SQ_INSTS_VALU counts the MFMAs too; the other VALU instructions occupy the SIMD's
+                      # vector pipe >= 4 cycles each (transcendentals 8), per SIMD-cycle of the launch
+                      "valu_insts": ctr[j].get("SQ_INSTS_VALU", 0), "lds_insts": ctr[j].get("SQ_INSTS_LDS", 0),
+                      "valu_pipe_share_min": round(4 * (ctr[j].get("SQ_INSTS_VALU", 0) - ctr[j].get("SQ_INSTS_MFMA", 0))
+                                                   / max(ctr[j].get("GRBM_GUI_ACTIVE", 1) / N_XCD * N_SIMD, 1), 3)})
     res = {
         "config": cfg, "B": B, "rows": rows_n, "H": H, "d": d, "C": C, "dtype": dtype,
         "source": "rocprofv3 --kernel-trace (durations) and three --pmc passes (FETCH_SIZE | WRITE_SIZE | "
@@ -112,6 +117,11 @@ def main(cfg, B, H, d, C, dtype, out=None):
         "mfma_busy_time_weighted": round(sum(b * x for b, x in zip(busy, dur)) / t, 3),
         "per_launch": table,
     }
+    sha = f"{base}_lib.sha256"  # tools/gpu.sh upmc: the library the passes ran on
+    try:
+        res["lib_sha256"] = open(sha).read().split()[0]
+    except OSError:
+        pass
     s = json.dumps(res, indent=1)
     if out:
         open(out, "w").write(s)
