@@ -122,7 +122,13 @@ MPCD_DEV f32x4 mfma_agpr1(const u32x4 &w, const u32x4 &x, f32x4 acc)
 #ifndef MPCD_RW_EXP_BAR2
 #define MPCD_RW_EXP_BAR2 0
 #endif
-#if !defined(MPCD_VARIANT) && (MPCD_RW_EXP_NOLASTEPI || MPCD_RW_EXP_BAR2 || defined(MPCD_PROF_FINAL_MFMA_ONLY))
+// MPCD_RW_EXP_NOVM: the streamed layers' buffer descriptor has zero records (every streamed weight load returns 0
+// without a memory access): the cost of the per-step weight stream, read as cycles per step in an MPCD_PROF_LAYERS
+// build (zero operands also raise the clock, so wall time would overstate it)
+#ifndef MPCD_RW_EXP_NOVM
+#define MPCD_RW_EXP_NOVM 0
+#endif
+#if !defined(MPCD_VARIANT) && (MPCD_RW_EXP_NOLASTEPI || MPCD_RW_EXP_BAR2 || MPCD_RW_EXP_NOVM || defined(MPCD_PROF_FINAL_MFMA_ONLY))
 #error "wrong-result timing switches build only as an experiment variant (build.py variant: -DMPCD_VARIANT)"
 #endif
 
@@ -167,8 +173,8 @@ struct MlpRw {
     {
         const uint64_t a = (uint64_t)wp;
         const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-        return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(woffx<D0>(NLAYER) * 4),
-                                                 0x00020000);
+        return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0,
+                                                 MPCD_RW_EXP_NOVM ? 0 : (int)(woffx<D0>(NLAYER) * 4), 0x00020000);
     }
 
     // streamed fragments of layer l for this wave
