@@ -53,6 +53,23 @@ MPCD_DEV f32x4 mfma_x3_agpr(const u32x4 &w0, const u32x4 &w1, const u32x4 &w2, c
     return acc;
 }
 
+// Transcendental pairs for packed consumers: both issued, then 2 wait states before a packed op may read them (a
+// packed read one wait state behind a v_exp / v_rcp gave wrong results on gfx950: unet_fused.hip exp2_pair,
+// profiles/r3_hazard_ab.txt). The same instructions as __builtin_amdgcn_exp2f / rcpf: the same bits.
+MPCD_DEV f32x2 exp2_pair(f32x2 z)
+{
+    float a, b;
+    asm("v_exp_f32 %0, %2\n\tv_exp_f32 %1, %3\n\ts_nop 1" : "=&v"(a), "=&v"(b) : "v"(z[0]), "v"(z[1]));
+    return f32x2{a, b};
+}
+MPCD_DEV f32x2 rcp_pair(f32x2 x)
+{
+    float a, b;
+    asm("v_rcp_f32 %0, %2\n\tv_rcp_f32 %1, %3\n\ts_nop 1" : "=&v"(a), "=&v"(b) : "v"(x[0]), "v"(x[1]));
+    return f32x2{a, b};
+}
+MPCD_DEV f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 // partial product m of a 32-k chunk, smallest first (mlp_x3.h mfma_x3): weight plane, activation plane
 constexpr int wpl(int m) { return m == 0 ? 2 : (m == 1 || m == 3) ? 1 : 0; }
 constexpr int xpl(int m) { return (m == 0 || m == 3 || m == 5) ? 0 : (m == 1 || m == 4) ? 1 : 2; }
@@ -102,6 +119,12 @@ MPCD_DEV f32x4 mfma_agpr1(const u32x4 &w, const u32x4 &x, f32x4 acc)
 // MFMA slots
 #ifndef MPCD_RW_TABLE_SIDE
 #define MPCD_RW_TABLE_SIDE 1
+#endif
+// MPCD_RW_PKTAIL = 1 (default): the exposed epilogue of a layer's last pass (nothing left to hide it under) with two
+// values per packed instruction (v_pk_mul / v_pk_add / v_pk_fma_f32, the same roundings) instead of the fenced scalar
+// micro-steps: loop VALU 1,631 -> 1,459 per wave-step, kernel -0.5 % (profiles/r6_mlp_tuning_ab.txt)
+#ifndef MPCD_RW_PKTAIL
+#define MPCD_RW_PKTAIL 1
 #endif
 // MPCD_RW_XREG = 1 (default): each lane keeps its x_t quads in registers across steps (the fp32 copy in LDS goes),
 // and the update's x-only products (a x, c2 x, std z) are formed while the final layer's operand reads are in
@@ -452,11 +475,43 @@ struct MlpRw {
             ev = acc;
             acc = nxt;
         }
+        // the last pass's epilogue, exposed (MPCD_RW_PKTAIL: packed, two values per instruction; epi_step's operations)
+        auto epi_tail = [&](int p) {
+            f32x2 a = {ev[0], ev[1]}, b = {ev[2], ev[3]};
+            if constexpr (EPI != EPI_NONE) {
+                const f32x2 l2e = {1.44269504088896341f, 1.44269504088896341f}, two = {2.0f, 2.0f};
+                const f32x2 m2 = {-2.0f, -2.0f}, one = {1.0f, 1.0f};
+                f32x2 ta = exp2_pair(a * l2e), tb = exp2_pair(b * l2e);
+                ta = fma2(ta, ta + two, two);
+                tb = fma2(tb, tb + two, two);
+                ta = fma2(m2, rcp_pair(ta), one);
+                tb = fma2(m2, rcp_pair(tb), one);
+                a = a * ta;
+                b = b * tb;
+            }
+            const int n = nt_of<l>(wave, jp(p)) * 16 + 4 * q;
+            const int ro = ct_of<l>(wave, cp(p)) * 16 + col;
+            char *o = lds + L::out_off(l) + ro * L::out_rs(l) + st_off(n, q, ro);
+            const u32x2 q0 = {pk_bf16(a[0], a[1]), pk_bf16(b[0], b[1])};
+            *reinterpret_cast<u32x2 *>(o) = q0;
+            a = a - f32x2{bf_lo(q0.x), bf_hi(q0.x)};
+            b = b - f32x2{bf_lo(q0.y), bf_hi(q0.y)};
+            const u32x2 q1 = {pk_bf16(a[0], a[1]), pk_bf16(b[0], b[1])};
+            *reinterpret_cast<u32x2 *>(o + L::out_pl(l)) = q1;
+            a = a - f32x2{bf_lo(q1.x), bf_hi(q1.x)};
+            b = b - f32x2{bf_lo(q1.y), bf_hi(q1.y)};
+            *reinterpret_cast<u32x2 *>(o + 2 * L::out_pl(l)) = u32x2{pk_bf16(a[0], a[1]), pk_bf16(b[0], b[1])};
+        };
         // MPCD_RW_EXP_NOLASTEPI (timing experiment only, wrong results): drop the exposed last-pass epilogue of
         // the multi-pass layers - the bound on what deferring it into the next layer could gain
-        if (!(MPCD_RW_EXP_NOLASTEPI && NP >= 2))
+        if (!(MPCD_RW_EXP_NOLASTEPI && NP >= 2)) {
+            if constexpr (MPCD_RW_PKTAIL) {
+                epi_tail(NP - 1);
+            } else {
 #pragma unroll
-            for (int u = 0; u < NSTEP; ++u) epi_step(u, NP - 1);
+                for (int u = 0; u < NSTEP; ++u) epi_step(u, NP - 1);
+            }
+        }
 #pragma unroll
         for (int k = NI * 6; k < NS; ++k) side(k);
 #else
