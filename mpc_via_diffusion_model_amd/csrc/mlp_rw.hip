@@ -923,7 +923,12 @@ struct MlpRw {
         for (int j = 0; j < 6; ++j)
             for (int i = threadIdx.x; i < A::N[2 * j + 1]; i += RW_T)
                 bic[cond_off(j) + i] = wp[woffx<D0>(2 * j + 1) + wfl<D0>(2 * j + 1) + i];
-        for (int i = threadIdx.x; i < COND_TOTAL; i += RW_T) cps[i] = CTX ? p.cproj[i] : 0.f;
+        // mpcd_mpc_step (ctx_fused): the shared context row's projection computed here, as ctx_prologue_row_kernel
+        // would (the same function: the same bits), so the control step has no prologue launch
+        for (int i = threadIdx.x; i < COND_TOTAL; i += RW_T)
+            cps[i] = !CTX ? 0.f
+                          : p.ctx_fused ? ctx_proj_col(p.ctx_row, p.ctx_dim, p.cond_layers, p.n_cond, p.cond_dim, i)
+                                        : p.cproj[i];
         if (threadIdx.x < CPW) reinterpret_cast<uint32_t *>(lds + L::AMX)[threadIdx.x] = 0u;
         uint32_t am[2] = {0u, 0u};
         for (int i = threadIdx.x; i < CPW * QUADS; i += RW_T) {  // x_T (fp32 + planes)

@@ -414,7 +414,10 @@ struct MlpX3 {
         for (int j = 0; j < 6; ++j)
             for (int i = threadIdx.x; i < A::N[2 * j + 1]; i += NTHR)
                 bic[cond_off(j) + i] = wp[woffx<D0>(2 * j + 1) + wfl<D0>(2 * j + 1) + i];
-        for (int i = threadIdx.x; i < COND_TOTAL; i += NTHR) cps[i] = CTX ? p.cproj[i] : 0.f;
+        for (int i = threadIdx.x; i < COND_TOTAL; i += NTHR)  // ctx_fused: as mlp_rw.hip
+            cps[i] = !CTX ? 0.f
+                          : p.ctx_fused ? ctx_proj_col(p.ctx_row, p.ctx_dim, p.cond_layers, p.n_cond, p.cond_dim, i)
+                                        : p.cproj[i];
         if (threadIdx.x < CPW) reinterpret_cast<uint32_t *>(lds + L::AMX)[threadIdx.x] = 0u;
         uint32_t am[2] = {0u, 0u};
         // x_T (fp32 + planes)

@@ -662,13 +662,16 @@ static int sample_impl(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr,
     }
     const float *cproj = nullptr;
     int64_t cstride = 0;
-    const bool fuse_ctx = ctx_row && d.kind == MPCD_NET_MLP && mlp_kernel_of(c, a->sampler, true) == MLPK_H2;
+    // the MLP samplers with a shared context (fp16 two-term and split-bf16; not the exact-f32 kernel, which stages
+    // per-candidate projections) compute mpcd_mpc_step's row projection in their own staging: one launch fewer
+    const int mk = d.kind == MPCD_NET_MLP ? mlp_kernel_of(c, a->sampler, true) : -1;
+    const bool fuse_ctx = ctx_row && (mk == MLPK_H2 || mk == MLPK_X3);
     if (d.context_dim > 0) {
         const bool shared = ctx_row || a->context_shared;
         const int64_t rows = shared ? 1 : a->batch;
         if ((rc = c->cproj.ensure(sizeof(float) * (size_t)rows * c->cond_total))) return rc;
         if (fuse_ctx) {
-            // the fp16 MLP kernel computes the row's projection in its own staging: one launch fewer
+            // computed by the sampler launch itself (ctx_proj_col)
         } else if (ctx_row)
             launch_ctx_prologue_row(*ctx_row, d.context_dim, cl, c->n_cond, c->cond_dim, c->cond_total,
                                     c->cproj.as<float>(), st);
