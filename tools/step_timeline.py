@@ -36,7 +36,7 @@ def main():
         prev_end = rows[a][0]
         for i in range(a, b):
             s, e, n = rows[i]
-            short = n.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+            short = n.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
             segs.setdefault(f"gap before {short}", []).append((s - prev_end) / 1e3 if i > a else 0.0)
             segs.setdefault(f"kernel {short}", []).append((e - s) / 1e3)
             prev_end = e
