@@ -390,6 +390,9 @@ int mpcd_unet_form(mpcd_ctx *ctx, int32_t sampler, int32_t out[4]);
 /* Timing of the last mpcd_sample's main kernel (HIP events on the call's stream), milliseconds.
  * Blocks until that kernel has finished. */
 int mpcd_last_sample_ms(mpcd_ctx *ctx, float *ms);
+/* Mean of that timing over the last n sample calls (1 <= n <= 256 and <= the calls made): a timed control loop reads
+ * it once afterwards instead of one mpcd_last_sample_ms per step. Blocks until the last of them has finished. */
+int mpcd_sample_ms_mean(mpcd_ctx *ctx, int32_t n, float *ms);
 
 #ifdef __cplusplus
 }

@@ -87,6 +87,7 @@ EXPORTS = {
     "mpcd_argmin": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                      ctypes.c_void_p], ctypes.c_int),
     "mpcd_last_sample_ms": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+    "mpcd_sample_ms_mean": ([ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
     "mpcd_clip_flags": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                          ctypes.c_void_p], ctypes.c_int),
     "mpcd_normalize_states": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,

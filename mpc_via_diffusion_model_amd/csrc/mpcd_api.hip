@@ -280,6 +280,11 @@ struct mpcd_ctx {
     bool plan_cached_valid = false;
     hipStream_t plan_stream = nullptr;  // stream the cached plan / tproj were produced on
     hipEvent_t plan_ev = nullptr;       // recorded after they were produced
+    // the timing events of the last kEvRing sample calls (ev0 / ev1: the latest pair): a control loop reads the mean
+    // kernel time once after its timed steps (mpcd_sample_ms_mean) instead of one host query per step
+    static constexpr int kEvRing = 256;
+    hipEvent_t evr[2][kEvRing] = {};
+    uint32_t ev_n = 0;  // sample calls recorded
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     float *dbg = nullptr;  // debug dump target for mpcd_eps (mpcd_debug_set)
@@ -547,11 +552,19 @@ int mpcd_create(int device, mpcd_ctx **out)
     DEVICE_GUARD(device);
     auto *c = new mpcd_ctx();
     c->device = device;
-    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipEventCreateWithFlags(&c->plan_ev, hipEventDisableTiming) != hipSuccess) {
+    bool ev_ok = hipEventCreateWithFlags(&c->plan_ev, hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; i < mpcd_ctx::kEvRing && ev_ok; ++i)
+        ev_ok = hipEventCreate(&c->evr[0][i]) == hipSuccess && hipEventCreate(&c->evr[1][i]) == hipSuccess;
+    if (!ev_ok) {
+        for (int i = 0; i < mpcd_ctx::kEvRing; ++i)
+            for (int j = 0; j < 2; ++j)
+                if (c->evr[j][i]) (void)hipEventDestroy(c->evr[j][i]);
+        if (c->plan_ev) (void)hipEventDestroy(c->plan_ev);
         delete c;
         return fail(MPCD_EHIP, "hipEventCreate failed");
     }
+    c->ev0 = c->evr[0][0];
+    c->ev1 = c->evr[1][0];
     if (int rc = c->flag.ensure(256)) {
         delete c;
         return rc;
@@ -572,8 +585,9 @@ void mpcd_destroy(mpcd_ctx *c)
     for (DevBuf *b : {&c->params, &c->wpack, &c->wpack3, &c->wpackh, &c->cond_layers, &c->unet_pack, &c->plan, &c->tproj, &c->cproj, &c->flag,
                       &c->unet_ws, &c->step_ctx, &c->step_part, &c->step_out, &c->step_amax})
         b->release();
-    if (c->ev0) (void)hipEventDestroy(c->ev0);
-    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (int i = 0; i < mpcd_ctx::kEvRing; ++i)
+        for (int j = 0; j < 2; ++j)
+            if (c->evr[j][i]) (void)hipEventDestroy(c->evr[j][i]);
     if (c->plan_ev) (void)hipEventDestroy(c->plan_ev);
     delete c->comm;
     if (c->step_host) (void)hipHostFree(c->step_host);
@@ -683,6 +697,8 @@ static int sample_impl(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr,
         cstride = shared ? 0 : c->cond_total;
     }
     const float wp1 = (float)(1.0 + a->w), wf = (float)a->w;
+    c->ev0 = c->evr[0][c->ev_n % mpcd_ctx::kEvRing];
+    c->ev1 = c->evr[1][c->ev_n % mpcd_ctx::kEvRing];
     HIP_TRY(hipEventRecord(c->ev0, st));
     if (d.kind == MPCD_NET_MLP) {
         MlpSampleArgs m{};
@@ -742,6 +758,7 @@ static int sample_impl(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr,
     }
     HIP_TRY(hipEventRecord(c->ev1, st));
     c->timed = true;
+    ++c->ev_n;
     return MPCD_OK;
 }
 
@@ -901,6 +918,24 @@ int mpcd_last_sample_ms(mpcd_ctx *c, float *ms)
     if (!c->timed) return fail(MPCD_ESTATE, "no sample call recorded");
     HIP_TRY(hipEventSynchronize(c->ev1));
     HIP_TRY(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return MPCD_OK;
+}
+
+int mpcd_sample_ms_mean(mpcd_ctx *c, int32_t n, float *ms)
+{
+    if (!c || !ms) return fail(MPCD_EINVAL, "null argument");
+    if (n < 1 || (uint32_t)n > c->ev_n || n > mpcd_ctx::kEvRing)
+        return fail(MPCD_EINVAL, "mpcd_sample_ms_mean: %d calls asked, %u recorded, at most %d kept", n, c->ev_n,
+                    mpcd_ctx::kEvRing);
+    HIP_TRY(hipEventSynchronize(c->ev1));
+    double sum = 0.0;
+    for (int k = 0; k < n; ++k) {
+        const int i = (int)((c->ev_n - 1 - (uint32_t)k) % mpcd_ctx::kEvRing);
+        float t = 0.f;
+        HIP_TRY(hipEventElapsedTime(&t, c->evr[0][i], c->evr[1][i]));
+        sum += t;
+    }
+    *ms = (float)(sum / n);
     return MPCD_OK;
 }
 

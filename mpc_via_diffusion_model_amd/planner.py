@@ -378,6 +378,12 @@ class DiffusionMPC:
         N.check(self._lib.mpcd_last_sample_ms(self._ctx, ctypes.byref(ms)), "mpcd_last_sample_ms")
         return ms.value
 
+    def sample_ms_mean(self, n):
+        """Mean sampler-kernel time (HIP events) over the last n sample calls (n <= 256), read once after a loop."""
+        ms = ctypes.c_float()
+        N.check(self._lib.mpcd_sample_ms_mean(self._ctx, int(n), ctypes.byref(ms)), "mpcd_sample_ms_mean")
+        return ms.value
+
     # ------------------------------------------------------------------ rollout / cost / selection (A13-A15)
     def rollout_cost(self, system: System, x0, u_norm, clip_flag=None):
         """fp64 cost per candidate [B] on device."""

@@ -228,3 +228,23 @@ def test_every_workgroup_layout_bit_identical(B, H, d, nwo, mode):
     assert torch.isfinite(ref).all()
     for lay, o in outs.items():
         assert torch.equal(o, ref), f"{lay} differs from 32x8 ({mode}, B={B}, H={H}): max |d| {float((o - ref).abs().max()):.3e}"
+
+
+def test_sample_ms_mean_is_the_mean_of_the_per_call_timings():
+    """mpcd_sample_ms_mean (the bench's one read after its timed loop) = the mean of mpcd_last_sample_ms over the
+    same calls; asking for more calls than were made is refused."""
+    from mpc_via_diffusion_model_amd._native import MpcdError
+
+    net = make_mlp(2, 16, 4, seed=5)
+    plan = _planner(net, 2, 16, 4, n_steps=50, dtype="f32x3")
+    with pytest.raises(MpcdError):
+        plan.sample_ms_mean(1)
+    ctx = _ctx(1, 4, True)
+    per_call = []
+    for i in range(5):
+        plan.sample_trajectories(ctx, 64, 16, w=0.01, seed=i)
+        per_call.append(plan.last_sample_ms())
+    assert plan.sample_ms_mean(5) == pytest.approx(float(np.mean(per_call)), rel=1e-5)
+    assert plan.sample_ms_mean(2) == pytest.approx(float(np.mean(per_call[-2:])), rel=1e-5)
+    with pytest.raises(MpcdError):
+        plan.sample_ms_mean(6)
