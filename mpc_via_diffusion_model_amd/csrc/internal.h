@@ -1,5 +1,6 @@
 // Internal (non-ABI) declarations shared by the libmpcd.so translation units.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -72,6 +73,20 @@ inline hipError_t allow_max_lds()
     return err[dev];
 }
 int device_cu_count();
+
+// The sample call's timing events handed to the MLP sampler's one launch: hipExtLaunchKernel records them as part of
+// that dispatch, so no hipEventRecord call sits on the host path in front of the launch (sample_impl sets them for the
+// launch and clears them after; null otherwise)
+struct LaunchEvents {
+    hipEvent_t start, stop;
+};
+extern thread_local LaunchEvents g_launch_ev;
+template <typename K, typename A>
+inline hipError_t launch_sampler_kernel(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const A &args)
+{
+    hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, stream, g_launch_ev.start, g_launch_ev.stop, 0u, args);
+    return hipGetLastError();
+}
 
 struct MlpSampleArgs {
     const float *wpack;      // packed linear layers (see mlp_sampler.hip)

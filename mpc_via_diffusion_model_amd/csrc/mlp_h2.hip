@@ -748,8 +748,7 @@ hipError_t launch_h2_r(const MlpSampleArgs &a, hipStream_t stream)
     static_assert(L::total <= 160 * 1024, "LDS budget (160 KiB per CU)");
     if (hipError_t e = allow_max_lds<&mlp_h2_kernel<D0, SMODE, CTX, R>>(); e != hipSuccess) return e;
     const int64_t blocks = (a.batch + L::CPW - 1) / L::CPW;
-    hipLaunchKernelGGL((mlp_h2_kernel<D0, SMODE, CTX, R>), dim3((unsigned)blocks), dim3(H2_T), (size_t)L::total, stream, a);
-    return hipGetLastError();
+    return launch_sampler_kernel(mlp_h2_kernel<D0, SMODE, CTX, R>, dim3((unsigned)blocks), dim3(H2_T), (size_t)L::total, stream, a);
 }
 
 template <int D0, int SMODE, bool CTX>

@@ -1150,8 +1150,7 @@ hipError_t launch_rw_r(const MlpSampleArgs &a, hipStream_t stream)
     static_assert(L::total <= 160 * 1024, "LDS budget (160 KiB per CU)");
     if (hipError_t e = allow_max_lds<&mlp_rw_kernel<D0, SMODE, CTX, R>>(); e != hipSuccess) return e;
     const int64_t blocks = (a.batch + L::CPW - 1) / L::CPW;
-    hipLaunchKernelGGL((mlp_rw_kernel<D0, SMODE, CTX, R>), dim3((unsigned)blocks), dim3(RW_T), (size_t)L::total, stream, a);
-    return hipGetLastError();
+    return launch_sampler_kernel(mlp_rw_kernel<D0, SMODE, CTX, R>, dim3((unsigned)blocks), dim3(RW_T), (size_t)L::total, stream, a);
 }
 
 template <int D0, int SMODE, bool CTX>

@@ -537,8 +537,7 @@ hipError_t launch_impl(const MlpSampleArgs &a, hipStream_t stream)
     const size_t lds_bytes = sizeof(float) * L::total(CTX);
     if (hipError_t e = allow_max_lds<&mlp_sample_kernel<D0, SMODE, CTX>>(); e != hipSuccess) return e;
     const int64_t blocks = (a.batch + L::CPW - 1) / L::CPW;
-    hipLaunchKernelGGL((mlp_sample_kernel<D0, SMODE, CTX>), dim3((unsigned)blocks), dim3(THREADS), lds_bytes, stream, a);
-    return hipGetLastError();
+    return launch_sampler_kernel(mlp_sample_kernel<D0, SMODE, CTX>, dim3((unsigned)blocks), dim3(THREADS), lds_bytes, stream, a);
 }
 
 template <int D0>

@@ -587,9 +587,7 @@ hipError_t launch_x3_r(const MlpSampleArgs &a, hipStream_t stream)
     static_assert(L::total <= 160 * 1024, "LDS budget (160 KiB per CU)");
     if (hipError_t e = allow_max_lds<&mlp_x3_kernel<D0, SMODE, CTX, R, W>>(); e != hipSuccess) return e;
     const int64_t blocks = (a.batch + L::CPW - 1) / L::CPW;
-    hipLaunchKernelGGL((mlp_x3_kernel<D0, SMODE, CTX, R, W>), dim3((unsigned)blocks), dim3(64 * W), (size_t)L::total, stream,
-                       a);
-    return hipGetLastError();
+    return launch_sampler_kernel(mlp_x3_kernel<D0, SMODE, CTX, R, W>, dim3((unsigned)blocks), dim3(64 * W), (size_t)L::total, stream, a);
 }
 
 // Workgroup layout (rows x waves): 32x8 (one per CU), 16x8 when 32-row workgroups would leave CUs idle

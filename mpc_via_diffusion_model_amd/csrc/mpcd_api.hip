@@ -512,6 +512,11 @@ hipError_t launch_mlp(mpcd_ctx *c, MlpSampleArgs &m, int nb, hipStream_t st)
 }
 }  // namespace
 
+#ifndef MPCD_SEPARATE_EVENT_RECORDS
+#define MPCD_SEPARATE_EVENT_RECORDS 0
+#endif
+thread_local LaunchEvents g_launch_ev{};
+
 extern "C" {
 
 const char *mpcd_last_error(void) { return g_err.c_str(); }
@@ -699,7 +704,9 @@ static int sample_impl(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr,
     const float wp1 = (float)(1.0 + a->w), wf = (float)a->w;
     c->ev0 = c->evr[0][c->ev_n % mpcd_ctx::kEvRing];
     c->ev1 = c->evr[1][c->ev_n % mpcd_ctx::kEvRing];
-    HIP_TRY(hipEventRecord(c->ev0, st));
+    // the MLP sampler's launch records both events itself (MPCD_SEPARATE_EVENT_RECORDS: separate records, A/B build)
+    constexpr bool kExtEv = !MPCD_SEPARATE_EVENT_RECORDS;
+    if (d.kind != MPCD_NET_MLP || !kExtEv) HIP_TRY(hipEventRecord(c->ev0, st));
     if (d.kind == MPCD_NET_MLP) {
         MlpSampleArgs m{};
         m.dbg = c->dbg;  // read only by the MPCD_PROF_LAYERS experiment build
@@ -728,7 +735,10 @@ static int sample_impl(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr,
             m.n_cond = c->n_cond;
             m.cond_dim = c->cond_dim;
         }
-        HIP_TRY(launch_mlp(c, m, cfg ? 2 : 1, st));
+        if (kExtEv) g_launch_ev = LaunchEvents{c->ev0, c->ev1};
+        const hipError_t le = launch_mlp(c, m, cfg ? 2 : 1, st);
+        g_launch_ev = LaunchEvents{};
+        HIP_TRY(le);
     } else {
         UnetSampleArgs u{};
         u.plan = c->plan.as<StepPlan>();
@@ -756,7 +766,7 @@ static int sample_impl(mpcd_ctx *c, const mpcd_sample_args *a, void *stream_ptr,
         rc = unet_sample(d, c->unet, u, st);
         if (rc) return fail(rc, "unet_sample: %s", unet_last_error());
     }
-    HIP_TRY(hipEventRecord(c->ev1, st));
+    if (d.kind != MPCD_NET_MLP || !kExtEv) HIP_TRY(hipEventRecord(c->ev1, st));
     c->timed = true;
     ++c->ev_n;
     return MPCD_OK;
